@@ -1,0 +1,218 @@
+"""Generate golden vectors by importing the reference itself (build container only).
+
+TEST INFRASTRUCTURE ONLY. Run from the repo root:
+
+    PYTHONDONTWRITEBYTECODE=1 python oracle/gen_golden.py
+
+It imports the reference modules from ``/root/reference`` (read-only; hence no bytecode) with a
+``pygame`` stub for the two panel modules that import pygame at the top
+(professional_meters.py:6, chromagram.py:8) -- no drawing code runs. Nothing of the reference is
+copied: only inputs and the reference's outputs are written, as small ``.npz`` files under
+``tests/golden/`` together with the numpy/scipy versions used (SURVEY.md §8(c) recipe).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+from types import SimpleNamespace
+
+import numpy as np
+import scipy
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+from oracle import signals as S  # noqa: E402
+
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+FS = 48000
+VERSIONS = np.array([np.__version__, scipy.__version__])
+
+
+def _import_reference():
+    sys.dont_write_bytecode = True
+    pg = types.ModuleType("pygame")
+    pg.font = SimpleNamespace(Font=object)
+    pg.Surface = object
+    sys.modules.setdefault("pygame", pg)
+    sys.path.insert(0, REF)
+    from omega4.audio.multi_resolution_fft import MultiResolutionFFT, FFTConfig
+    from omega4.panels.professional_meters import ProfessionalMetering
+    from omega4.audio.pipeline import AudioProcessingPipeline
+    from omega4.audio.audio_config import PipelineConfig
+    from omega4.optimization.freq_mapper import PrecomputedFrequencyMapper
+    from omega4.panels.chromagram import ChromagramAnalyzer
+    from omega4.optimization.batched_fft_processor import BatchedFFTProcessor
+    return SimpleNamespace(**locals())
+
+
+def _mrfft(R, configs=None):
+    m = R.MultiResolutionFFT(FS)
+    if configs is not None:
+        m.configs = [R.FFTConfig(*c) for c in configs]
+        m._setup_windows(); m._setup_buffers(); m._setup_frequency_arrays(); m._setup_working_arrays()
+    return m
+
+
+NS = [((20, 200), 16384, 1024, 1.5), ((200, 1000), 8192, 512, 1.2),
+      ((1000, 5000), 4096, 256, 1.0), ((5000, 20000), 1024, 256, 1.5)]
+
+
+def gen_mrfft(R):
+    d = {"versions": VERSIONS}
+    # default configs, fresh instance per frame, 2048- and 4096-sample chunks
+    cases = {"sine1k_2048": S.sine(1000, 0.5, 2048), "noise_2048": S.noise(0, 2048, 0.3),
+             "triad_4096": S.triad(4096, 0.3), "comp_4096": S.composite(4096),
+             "silence_4096": np.zeros(4096, np.float32), "sine50_8192": S.sine(50, 0.8, 8192)}
+    for name, x in cases.items():
+        m = _mrfft(R)
+        r = m.process_audio_chunk(x)
+        d[f"{name}/x"] = x
+        d[f"{name}/res"] = np.array(sorted(r.keys()))
+        for i, fr in r.items():
+            d[f"{name}/mag{i}"] = fr.magnitude
+        for T in (512, 1024):
+            c, t = m.combine_results_optimized(r, target_bins=T)
+            d[f"{name}/comb{T}"] = c
+            d[f"{name}/tgt{T}"] = t
+        r2 = _mrfft(R).process_audio_chunk(x, apply_weighting=False)
+        for i, fr in r2.items():
+            d[f"{name}/raw{i}"] = fr.magnitude
+    # north-star sizes on cfg2-style frames
+    xb = S.cfg2_batch(2)
+    for k, x in enumerate([xb[0, 0], xb[1, 1], S.triad(16384, 0.5)]):
+        m = _mrfft(R, NS)
+        r = m.process_audio_chunk(x)
+        d[f"ns{k}/x"] = x
+        for i, fr in r.items():
+            d[f"ns{k}/mag{i}"] = fr.magnitude
+        d[f"ns{k}/comb512"] = m.combine_results_optimized(r, target_bins=512)[0]
+    # stream layout: one instance fed 512-sample chunks (CircularBuffer semantics)
+    st = np.concatenate([S.sine(440, 0.25, 512 * 24) + S.noise(5, 512 * 24, 0.05)])
+    m = _mrfft(R)
+    res_sets, combs = [], []
+    for c in range(24):
+        r = m.process_audio_chunk(st[c * 512:(c + 1) * 512])
+        res_sets.append(sum(1 << i for i in r))
+        combs.append(m.combine_results_optimized(r, target_bins=512)[0] if r else np.zeros(512, np.float32))
+        if c == 23:
+            for i, fr in r.items():
+                d[f"stream/mag{i}"] = fr.magnitude
+    d["stream/x"] = st
+    d["stream/resmask"] = np.array(res_sets)
+    d["stream/comb512"] = np.array(combs, np.float32)
+    np.savez_compressed(os.path.join(OUT, "mrfft.npz"), **d)
+
+
+def _meter_run(R, frames):
+    pm = R.ProfessionalMetering(FS)
+    li, tp, agg = [], [], []
+    for x in frames:
+        w = pm.apply_weighting(x)
+        ms = np.mean(w ** 2)
+        li.append(-0.691 + 10 * np.log10(ms) if ms > 1e-10 else -100.0)
+        tp.append(pm.calculate_true_peak(x))
+        r = pm.calculate_lufs(x)
+        agg.append([r[k] for k in ("momentary", "short_term", "integrated", "range", "true_peak")])
+    return np.array(li), np.array(tp, np.float64), np.array(agg, np.float64)
+
+
+def gen_meters(R):
+    d = {"versions": VERSIONS}
+    seqs = {
+        "cfg2L": S.cfg2_batch(8)[:, 0],                                  # M = 16384
+        "sine2048": (S.sine(997, 0.25, 40 * 2048) + S.noise(11, 40 * 2048, 0.02)).reshape(40, 2048),
+        "low50_4096": S.sine(50, 0.5, 6 * 4096).reshape(6, 4096),
+        "silence": np.zeros((5, 2048), np.float32),
+        "steps1024": S.level_steps(300, 1024),
+        "square1024": np.stack([S.square(1024)] * 3),
+    }
+    for name, fr in seqs.items():
+        li, tp, agg = _meter_run(R, fr)
+        d[f"{name}/x"] = fr
+        d[f"{name}/lufs_inst"], d[f"{name}/tp"], d[f"{name}/agg"] = li, tp, agg
+    # long stream past the 3600-frame integrated window: inputs regenerated from signals.level_steps
+    li, tp, agg = _meter_run(R, S.level_steps(3700, 512, seed=9))
+    d["long/lufs_inst"], d["long/tp"], d["long/agg"] = li, tp, agg
+    # the weighting filter output itself and the reference test signals of odd lengths
+    pm = R.ProfessionalMetering(FS)
+    for name, x in {"comp4800": S.composite(4800), "square480": S.square(480),
+                    "sine2048": S.sine(1000, 0.1, 2048), "hann2048_f64": (S.composite(2048) * np.hanning(2048))}.items():
+        d[f"kw/{name}/x"] = x
+        d[f"kw/{name}/y"] = pm.apply_k_weighting(x)
+        d[f"kw/{name}/tp"] = np.float64(pm.calculate_true_peak(x))
+    kf = pm.k_weighting_filter
+    d["coef/hp_b"], d["coef/hp_a"], d["coef/sh_b"], d["coef/sh_a"] = kf["hp_b"], kf["hp_a"], kf["shelf_b"], kf["shelf_a"]
+    np.savez_compressed(os.path.join(OUT, "meters.npz"), **d)
+
+
+def gen_bands(R):
+    d = {"versions": VERSIONS}
+    xb = S.cfg3_batch(4)
+    mags = np.stack([np.abs(np.fft.rfft(x * np.blackman(8192).astype(np.float32))) for x in xb]).astype(np.float32)
+    d["mags8192"] = mags
+    for nb, fft in ((512, 8192), (768, 4096)):
+        cfg = R.PipelineConfig(num_bands=nb, fft_size=fft, ring_buffer_size=fft * 4)
+        p = R.AudioProcessingPipeline(cfg)
+        d[f"pipe{nb}_{fft}/starts"] = np.array(p.band_indices["starts"])
+        d[f"pipe{nb}_{fft}/ends"] = np.array(p.band_indices["ends"])
+        d[f"pipe{nb}_{fft}/comp"] = p.freq_compensation
+        src = mags if fft == 8192 else mags[:, : fft // 2 + 1]
+        d[f"pipe{nb}_{fft}/out"] = np.stack([p.map_to_bands(m, apply_smoothing=False) for m in src])
+        d[f"pipe{nb}_{fft}/smooth"] = np.stack([p.map_to_bands(m, apply_smoothing=True) for m in src])
+    for fft, nb in ((2048, 512), (8192, 512)):
+        fm = R.PrecomputedFrequencyMapper(FS, fft, nb)
+        d[f"mel{fft}_{nb}/bands"] = np.array(fm.mapping.band_indices)
+        d[f"mel{fft}_{nb}/comp"] = fm.mapping.compensation_curve
+        spec = mags[:, : fft // 2 + 1]
+        d[f"mel{fft}_{nb}/spec"] = spec
+        d[f"mel{fft}_{nb}/out_comp"] = np.stack([fm.map_spectrum_to_bars(s, True) for s in spec])
+        d[f"mel{fft}_{nb}/out_raw"] = np.stack([fm.map_spectrum_to_bars(s, False) for s in spec])
+        d[f"mel{fft}_{nb}/out_512in"] = np.stack([fm.map_spectrum_to_bars(s[:512], False) for s in spec])
+    np.savez_compressed(os.path.join(OUT, "bands.npz"), **d)
+
+
+def gen_chroma(R):
+    d = {"versions": VERSIONS}
+    xb = S.cfg3_batch(6)
+    mags = np.stack([np.abs(np.fft.rfft(x * np.blackman(8192).astype(np.float32))) for x in xb]).astype(np.float32)
+    freqs = np.fft.rfftfreq(8192, 1 / FS)
+    ca = R.ChromagramAnalyzer(FS)
+    d["mags"], d["freqs"] = mags, freqs
+    d["out"] = np.stack([ca.compute_chromagram(m, freqs) for m in mags])
+    # known answer: a 440 Hz sine gives chroma argmax 9 (A)
+    s = np.abs(np.fft.rfft(S.sine(440, 0.5, 8192) * np.blackman(8192).astype(np.float32))).astype(np.float32)
+    d["a440_mag"] = s
+    d["a440_out"] = R.ChromagramAnalyzer(FS).compute_chromagram(s, freqs)
+    np.savez_compressed(os.path.join(OUT, "chroma.npz"), **d)
+
+
+def gen_batched(R):
+    d = {"versions": VERSIONS}
+    bp = R.BatchedFFTProcessor()
+    reqs = []
+    x64 = S.composite(2048).astype(np.float64) * np.hanning(2048)  # app path: double Hann
+    for name, x, n, w in (("app_f64_2048_hann", x64, 2048, "hann"), ("f32_4096_blackman", S.noise(2, 4096, 0.1), 4096, "blackman"),
+                          ("pad_1000_1024_hamming", S.sine(440, 0.3, 1000), 1024, "hamming"),
+                          ("trim_20000_16384_hann", S.noise(4, 20000, 0.1), 16384, "hann")):
+        rid = bp.prepare_batch(name, x, n, w)
+        reqs.append((name, rid, x, n, w))
+    bp.process_batch()
+    res = bp.distribute_results()
+    for name, rid, x, n, w in reqs:
+        d[f"{name}/x"] = x
+        d[f"{name}/mag"] = res[rid]["magnitude"]
+        d[f"{name}/complex"] = res[rid]["complex"]
+    np.savez_compressed(os.path.join(OUT, "batched.npz"), **d)
+
+
+if __name__ == "__main__":
+    if not os.path.isdir(REF):
+        sys.exit("reference not present: golden vectors can only be generated in the build container")
+    os.makedirs(OUT, exist_ok=True)
+    R = _import_reference()
+    for g in (gen_mrfft, gen_meters, gen_bands, gen_chroma, gen_batched):
+        g(R)
+        print("wrote", g.__name__)

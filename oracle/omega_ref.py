@@ -1,0 +1,574 @@
+"""numpy/scipy restatement of the reference hot path (the parity oracle).
+
+TEST INFRASTRUCTURE ONLY -- see ``oracle/__init__.py``. The product path (``omega_gpu`` over
+``libomega.so``) never imports this module.
+
+Every function restates one reference function in a *stateless frame form*  and
+cites the reference ``file:line`` it follows (paths relative to the reference repo root). The
+arithmetic lives in numpy.fft (pocketfft) and scipy.signal, exactly as in the reference; both are
+third-party dependencies pinned here at numpy 2.2.6 / scipy 1.15.3 (``requirements.txt:3-4`` only
+says ``numpy>=1.21``, ``scipy>=1.7``). numpy >= 2 computes a float32 rfft in single precision;
+numpy < 2 would promote to float64 -- the golden fixtures record the versions they were made with.
+"""
+from __future__ import annotations
+
+from collections import deque
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import scipy.signal as _sig
+
+# ----------------------------------------------------------------------------------------------
+# A1: FFTConfig + windows + frequency arrays   (omega4/audio/multi_resolution_fft.py:26-44,
+#     :149-154, :171-193, :210-215)
+# ----------------------------------------------------------------------------------------------
+
+
+@dataclass(frozen=True)
+class FFTConfig:
+    """One resolution: (freq_range, fft_size, hop_size, weight); window is Blackman
+    (multi_resolution_fft.py:26-33; validation :35-44 is mirrored by the facade)."""
+
+    freq_range: Tuple[float, float]
+    fft_size: int
+    hop_size: int
+    weight: float
+    window: str = "blackman"
+
+
+# multi_resolution_fft.py:149-154
+DEFAULT_CONFIGS: Tuple[FFTConfig, ...] = (
+    FFTConfig((20, 200), 4096, 1024, 1.5),
+    FFTConfig((200, 1000), 2048, 512, 1.2),
+    FFTConfig((1000, 5000), 1024, 256, 1.0),
+    FFTConfig((5000, 20000), 1024, 256, 1.5),
+)
+
+# BASELINE.json north-star sizes over the same ranges and weights.
+NORTHSTAR_CONFIGS: Tuple[FFTConfig, ...] = (
+    FFTConfig((20, 200), 16384, 1024, 1.5),
+    FFTConfig((200, 1000), 8192, 512, 1.2),
+    FFTConfig((1000, 5000), 4096, 256, 1.0),
+    FFTConfig((5000, 20000), 1024, 256, 1.5),
+)
+
+
+def window_f32(n: int, kind: str = "blackman") -> np.ndarray:
+    """np.<window>(n) cast to float32 (multi_resolution_fft.py:177-188; batched_fft_processor.py:91-101)."""
+    if kind == "blackman":
+        w = np.blackman(n)
+    elif kind == "hann":
+        w = np.hanning(n)
+    elif kind == "hamming":
+        w = np.hamming(n)
+    else:  # 'rect' / unknown -> ones (batched_fft_processor.py:99-100)
+        w = np.ones(n)
+    return w.astype(np.float32)
+
+
+def rfft_freqs(n: int, fs: float) -> np.ndarray:
+    """np.fft.rfftfreq(n, 1/fs) (multi_resolution_fft.py:215)."""
+    return np.fft.rfftfreq(n, 1 / fs)
+
+
+# ----------------------------------------------------------------------------------------------
+# A4: psychoacoustic weights   (multi_resolution_fft.py:304-333)
+# ----------------------------------------------------------------------------------------------
+
+
+def psycho_weights(cfg: FFTConfig, fs: float) -> np.ndarray:
+    """Per-bin float32 weight table: fill(weight) then compounding products on inclusive masks,
+    only inside the inclusive [lo, hi] range (multi_resolution_fft.py:310-326)."""
+    freqs = rfft_freqs(cfg.fft_size, fs)
+    w = np.ones(cfg.fft_size // 2 + 1, dtype=np.float32)
+    w.fill(cfg.weight)
+    lo, hi = cfg.freq_range
+    rng = (freqs >= lo) & (freqs <= hi)
+    w[rng & (freqs >= 60) & (freqs <= 120)] *= 1.8
+    w[rng & (freqs >= 200) & (freqs <= 400)] *= 1.4
+    w[rng & (freqs >= 2000) & (freqs <= 5000)] *= 1.2
+    w[rng & (freqs >= 20) & (freqs <= 80)] *= 1.6
+    return w
+
+
+# ----------------------------------------------------------------------------------------------
+# A2 + A3: stateless multi-resolution FFT of one frame   (multi_resolution_fft.py:228-302)
+# ----------------------------------------------------------------------------------------------
+
+
+def mrfft_frame(x: np.ndarray, configs: Sequence[FFTConfig] = DEFAULT_CONFIGS, fs: float = 48000,
+                apply_weighting: bool = True) -> Dict[int, np.ndarray]:
+    """Magnitudes of a *fresh* MultiResolutionFFT fed one chunk ``x``.
+
+    A fresh CircularBuffer of size >= 2N holds the last min(len, size) samples; ``read_latest(N)``
+    returns None until N samples were written (:99-126), so resolution i exists iff len(x) >= N_i
+    and then sees the last N_i samples. Per resolution: float32 window
+    multiply (:268-269), np.fft.rfft (complex64 for float32 input on numpy >= 2, :272), np.abs
+    (:273), weighting (:276-279), fresh copy (:283).
+    """
+    x = np.asarray(x, dtype=np.float32)  # CircularBuffer is float32 (:55, :60)
+    out: Dict[int, np.ndarray] = {}
+    for i, cfg in enumerate(configs):
+        n = cfg.fft_size
+        if len(x) < n:
+            continue
+        windowed = np.multiply(x[-n:], window_f32(n, cfg.window))
+        mag = np.abs(np.fft.rfft(windowed))
+        if apply_weighting:
+            mag = mag * psycho_weights(cfg, fs)[: len(mag)]
+        out[i] = mag.copy()
+    return out
+
+
+class MRFFTStream:
+    """Stateful restatement of MultiResolutionFFT's per-resolution CircularBuffers
+    (multi_resolution_fft.py:52-133, :195-208) for the stream layout."""
+
+    def __init__(self, configs: Sequence[FFTConfig] = DEFAULT_CONFIGS, fs: float = 48000):
+        self.configs = list(configs)
+        self.fs = fs
+        self.bufs = [np.zeros(0, np.float32) for _ in configs]
+        self.sizes = [max(c.fft_size * 2, c.fft_size + c.hop_size) for c in configs]  # :202
+
+    def process(self, chunk: np.ndarray, apply_weighting: bool = True) -> Dict[int, np.ndarray]:
+        chunk = np.asarray(chunk, dtype=np.float32)
+        if len(chunk) == 0:  # :240-242
+            return {}
+        out = {}
+        for i, cfg in enumerate(self.configs):
+            self.bufs[i] = np.concatenate([self.bufs[i], chunk])[-self.sizes[i]:]
+            if len(self.bufs[i]) < cfg.fft_size:
+                continue
+            out.update({i: mrfft_frame(self.bufs[i], [cfg], self.fs, apply_weighting)[0]})
+        return out
+
+
+# ----------------------------------------------------------------------------------------------
+# A5: combine onto a linear target grid   (multi_resolution_fft.py:335-408)
+# ----------------------------------------------------------------------------------------------
+
+
+def combine(results: Dict[int, np.ndarray], configs: Sequence[FFTConfig] = DEFAULT_CONFIGS,
+            fs: float = 48000, max_freq: float = 20000, target_bins: int = 1024
+            ) -> Tuple[np.ndarray, np.ndarray]:
+    """Edge-clamped np.interp of each resolution's in-range bins onto linspace(0, max_freq, T),
+    weight-summed into float32 accumulators (zeroed pool arrays, array_pool.py:53) and divided
+    by the weight sum where it is > 0 (:393-395)."""
+    max_freq = min(max_freq, fs / 2)  # :146
+    target = np.linspace(0, max_freq, target_bins)
+    if not results:  # :347-349
+        return np.zeros(target_bins), target
+    acc = np.zeros(target_bins, np.float32)
+    wsum = np.zeros(target_bins, np.float32)
+    for i, mag in results.items():
+        cfg = configs[i]
+        freqs = rfft_freqs(cfg.fft_size, fs)
+        lo, hi = cfg.freq_range
+        valid = (freqs >= lo) & (freqs <= hi)
+        if not np.any(valid) or valid.sum() < 2:
+            continue
+        tmask = (target >= lo) & (target <= hi)
+        if not np.any(tmask):
+            continue
+        idx = np.where(tmask)[0]
+        interp = np.interp(target[tmask], freqs[valid], mag[valid])
+        acc[idx] += interp * cfg.weight
+        wsum[idx] += cfg.weight
+    ok = wsum > 0
+    acc[ok] /= wsum[ok]
+    return acc.copy(), target
+
+
+def combine_table(configs: Sequence[FFTConfig], fs: float, max_freq: float, target_bins: int):
+    """The per-target interpolation plan implied by :func:`combine` (host-side precompute the HIP
+    epilogue also uses): for each target bin, (resolution, lower bin, fraction) per owner."""
+    max_freq = min(max_freq, fs / 2)
+    target = np.linspace(0, max_freq, target_bins)
+    plan: List[List[Tuple[int, int, float]]] = [[] for _ in range(target_bins)]
+    for i, cfg in enumerate(configs):
+        freqs = rfft_freqs(cfg.fft_size, fs)
+        lo, hi = cfg.freq_range
+        vidx = np.where((freqs >= lo) & (freqs <= hi))[0]
+        if len(vidx) < 2:
+            continue
+        vf = freqs[vidx]
+        for t in np.where((target >= lo) & (target <= hi))[0]:
+            x = target[t]
+            if x <= vf[0]:
+                plan[t].append((i, int(vidx[0]), 0.0))
+            elif x >= vf[-1]:
+                plan[t].append((i, int(vidx[-1]), 0.0))
+            else:
+                j = int(np.searchsorted(vf, x, side="right") - 1)
+                plan[t].append((i, int(vidx[j]), float((x - vf[j]) / (vf[j + 1] - vf[j]))))
+    return plan
+
+
+# ----------------------------------------------------------------------------------------------
+# A6: K-weighting = 2 x filtfilt + blend   (omega4/panels/professional_meters.py:48-72, :129-153)
+# ----------------------------------------------------------------------------------------------
+
+
+def k_weighting_coeffs(fs: float = 48000):
+    """scipy butter(2, 38/nyq, 'high') and iirfilter(2, 1500/nyq, 'high', 'butter')
+    (professional_meters.py:50-64). ``shelf_gain`` (:59) is computed but never used."""
+    nyq = fs / 2
+    hp_b, hp_a = _sig.butter(2, 38 / nyq, btype="high")
+    sh_b, sh_a = _sig.iirfilter(2, 1500 / nyq, btype="high", ftype="butter", output="ba")
+    return hp_b, hp_a, sh_b, sh_a
+
+
+def lfilter_zi2(b, a) -> np.ndarray:
+    """Closed form of scipy.signal.lfilter_zi for a biquad (solve (I - companion(a).T) zi = B)."""
+    b0 = b[0]
+    B0 = b[1] - a[1] * b0
+    B1 = b[2] - a[2] * b0
+    z0 = (B0 + B1) / (1 + a[1] + a[2])
+    return np.array([z0, B1 - a[2] * z0])
+
+
+def odd_ext(x: np.ndarray, n: int) -> np.ndarray:
+    """scipy.signal._arraytools.odd_ext along the last axis."""
+    left = 2 * x[..., :1] - x[..., n:0:-1]
+    right = 2 * x[..., -1:] - x[..., -2:-(n + 2):-1]
+    return np.concatenate([left, x, right], axis=-1)
+
+
+def filtfilt(b, a, x: np.ndarray) -> np.ndarray:
+    """scipy.signal.filtfilt(b, a, x) with its defaults (padtype='odd', padlen=3*max(len(a),len(b))
+    = 9, method='pad'): DF2T lfilter forward from zi*ext[0], backward from zi*y[-1], then crop."""
+    edge = 3 * max(len(a), len(b))
+    x = np.asarray(x)
+    if x.shape[-1] <= edge:
+        raise ValueError("The length of the input vector x must be greater than padlen, which is %d." % edge)
+    ext = odd_ext(x, edge).astype(np.float64)  # the extension is formed in the input dtype
+    zi = _sig.lfilter_zi(b, a)
+    y, _ = _sig.lfilter(b, a, ext, zi=zi * ext[..., :1])
+    y, _ = _sig.lfilter(b, a, y[..., ::-1], zi=zi * y[..., -1:])
+    return y[..., ::-1][..., edge:-edge]
+
+
+def apply_k_weighting(x: np.ndarray, fs: float = 48000) -> np.ndarray:
+    """professional_meters.py:129-153: RMS gate (< 1e-6 -> zeros), HP38 filtfilt, shelf filtfilt,
+    y = f + 0.3 (s - f)."""
+    x = np.asarray(x)
+    if np.sqrt(np.mean(x ** 2)) < 1e-6:
+        return np.zeros_like(x)
+    hp_b, hp_a, sh_b, sh_a = k_weighting_coeffs(fs)
+    f = filtfilt(hp_b, hp_a, x)
+    s = filtfilt(sh_b, sh_a, f)
+    return f + (s - f) * 0.3
+
+
+def lufs_instant(x: np.ndarray, fs: float = 48000, weighting: str = "K") -> float:
+    """professional_meters.py:236-246 (instantaneous part of calculate_lufs)."""
+    y = apply_k_weighting(x, fs) if weighting == "K" else np.asarray(x)
+    ms = np.mean(y ** 2)
+    return float(-0.691 + 10 * np.log10(ms)) if ms > 1e-10 else -100.0
+
+
+# ----------------------------------------------------------------------------------------------
+# A8: true peak by 4x FFT resampling   (professional_meters.py:283-299; scipy.signal.resample)
+# ----------------------------------------------------------------------------------------------
+
+
+def resample_fft(x: np.ndarray, num: int) -> np.ndarray:
+    """scipy.signal.resample(x, num) for real 1-D x, no window: rfft, copy bins 0..N//2, halve an
+    even-length Nyquist bin when upsampling, irfft(num), scale num/len (dtype follows input)."""
+    x = np.asarray(x)
+    nx = len(x)
+    X = np.fft.rfft(x)
+    Y = np.zeros(num // 2 + 1, X.dtype)
+    n = min(num, nx)
+    Y[: n // 2 + 1] = X[: n // 2 + 1]
+    if n % 2 == 0:
+        if num < nx:
+            Y[n // 2] *= 2.0
+        elif nx < num:
+            Y[n // 2] *= 0.5
+    y = np.fft.irfft(Y, num)
+    y *= float(num) / float(nx)
+    return y
+
+
+def true_peak(x: np.ndarray, oversampling: int = 4) -> float:
+    """professional_meters.py:283-299: 20*log10(max|resample(x, 4M)|), -100 if peak < 1e-10 or empty."""
+    if len(x) == 0:
+        return -100.0
+    peak = np.max(np.abs(resample_fft(x, len(x) * oversampling)))
+    if peak < 1e-10:
+        return -100.0
+    return 20 * np.log10(peak)
+
+
+# ----------------------------------------------------------------------------------------------
+# A7 + A9: calculate_lufs with its frame-count deques   (professional_meters.py:16-46, :231-281)
+# ----------------------------------------------------------------------------------------------
+
+
+class MeterState:
+    """Per-stream state of ProfessionalMetering: 24/180/3600-deep LUFS deques and a 60-deep TP
+    deque (professional_meters.py:20-25), gate -70 (:36), current values (:39-45)."""
+
+    def __init__(self, fs: float = 48000):
+        self.fs = fs
+        self.mom = deque(maxlen=int(0.4 * 60))
+        self.short = deque(maxlen=int(3.0 * 60))
+        self.integ = deque(maxlen=int(60 * 60))
+        self.peaks = deque(maxlen=int(1.0 * 60))
+        self.gate = -70.0
+        self.current = {"momentary": -100.0, "short_term": -100.0, "integrated": -100.0,
+                        "range": 0.0, "true_peak": -100.0}
+
+    def update(self, x: np.ndarray, lufs_inst: Optional[float] = None,
+               tp: Optional[float] = None) -> Dict[str, float]:
+        """One calculate_lufs call. ``lufs_inst``/``tp`` may be injected (to score aggregates
+        against device-computed instantaneous values); otherwise computed from ``x``."""
+        if len(x) == 0:  # :233-234
+            return self.current
+        li = lufs_instant(x, self.fs) if lufs_inst is None else lufs_inst
+        self.mom.append(li)
+        self.short.append(li)
+        self.integ.append(li)
+        self.current["momentary"] = np.mean(self.mom)
+        self.current["short_term"] = np.mean(self.short)
+        gated = [v for v in self.integ if v > self.gate]
+        if gated:
+            self.current["integrated"] = np.mean(gated)
+            self.current["range"] = np.percentile(gated, 95) - np.percentile(gated, 10)
+        else:
+            self.current["integrated"] = -100.0
+            self.current["range"] = 0.0
+        self.peaks.append(true_peak(x) if tp is None else tp)
+        self.current["true_peak"] = max(self.peaks)
+        return self.current
+
+
+AGG_KEYS = ("momentary", "short_term", "integrated", "range", "true_peak")
+
+
+def meter_sequence(frames: np.ndarray, fs: float = 48000) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Run one stream of frames [F, M] through a fresh MeterState; returns (lufs_inst[F], tp[F],
+    aggregates[F, 5] in AGG_KEYS order)."""
+    st = MeterState(fs)
+    li = np.zeros(len(frames))
+    tp = np.zeros(len(frames))
+    agg = np.zeros((len(frames), 5))
+    for f, x in enumerate(frames):
+        li[f] = lufs_instant(x, fs)
+        tp[f] = true_peak(x)
+        d = st.update(x, li[f], tp[f])
+        agg[f] = [d[k] for k in AGG_KEYS]
+    return li, tp, agg
+
+
+# ----------------------------------------------------------------------------------------------
+# A10: perceptual log/linear bands, max-reduce   (omega4/audio/pipeline.py:145-230, :295-335)
+# ----------------------------------------------------------------------------------------------
+
+
+def pipeline_band_table(fs: float = 48000, num_bands: int = 768, fft_size: int = 4096,
+                        min_freq: float = 20.0, max_freq: float = 20000.0,
+                        transition: float = 1000.0, low_ratio: float = 0.5):
+    """(starts, ends, compensation) of AudioProcessingPipeline (pipeline.py:165-230, :145-163).
+    Only num_bands-1 bands exist (len(all_freqs) - 1)."""
+    nyq = fs / 2
+    width = nyq / (fft_size // 2)
+    max_f = min(max_freq, nyq)
+    tb = int(num_bands * low_ratio)
+    lows = np.logspace(np.log10(min_freq), np.log10(transition), tb)
+    highs = np.linspace(transition, max_f, num_bands - tb + 1)[1:]
+    allf = np.concatenate([lows, highs])
+    starts, ends, fs_, fe_ = [], [], [], []
+    for i in range(min(len(allf) - 1, num_bands)):
+        a, b = allf[i], allf[i + 1]
+        s, e = int(a / width), int(b / width)
+        if e <= s:
+            e = s + 1
+        s = max(0, min(s, fft_size // 2 - 1))
+        e = max(s + 1, min(e, fft_size // 2))
+        starts.append(s), ends.append(e), fs_.append(a), fe_.append(b)
+    centers = (np.array(fs_) + np.array(fe_)) / 2
+    comp = np.ones_like(centers)
+    comp[centers < 100] = 2.0
+    comp[(centers >= 100) & (centers < 250)] = 1.5
+    comp[(centers >= 250) & (centers < 1000)] = 1.2
+    comp[centers >= 10000] = 1.3
+    return np.array(starts), np.array(ends), comp
+
+
+def map_to_bands(mag: np.ndarray, starts, ends, comp, num_bands: int,
+                 smooth_state: Optional[np.ndarray] = None, smoothing: float = 0.7) -> np.ndarray:
+    """pipeline.py:295-335: v[i] = max(mag[s:e]) when the band fits, v[:len(comp)] *= comp, then
+    optionally s = 0.7 s + 0.3 v (in place on ``smooth_state``)."""
+    v = np.zeros(num_bands, np.float32)
+    if mag is None or len(mag) == 0:
+        return v
+    nvalid = min(num_bands, len(starts), len(ends))
+    for i in range(nvalid):
+        s, e = starts[i], ends[i]
+        if s < len(mag) and e <= len(mag):
+            v[i] = np.max(mag[s:e])
+    v[: len(comp)] *= comp
+    if smooth_state is not None:
+        smooth_state *= smoothing
+        smooth_state += (1 - smoothing) * v
+        return smooth_state.copy()
+    return v.copy()
+
+
+# ----------------------------------------------------------------------------------------------
+# A11: mel bands, mean-reduce   (omega4/optimization/freq_mapper.py:83-196)
+# ----------------------------------------------------------------------------------------------
+
+
+def mel_band_table(fs: float, fft_size: int, num_bars: int) -> List[Tuple[int, int]]:
+    """freq_mapper.py:83-124."""
+    width = fs / fft_size
+    hz_to_mel = lambda hz: 2595 * np.log10(1 + hz / 700)
+    mel_to_hz = lambda mel: 700 * (10 ** (mel / 2595) - 1)
+    mel = np.linspace(hz_to_mel(20), hz_to_mel(20000), num_bars + 1)
+    fp = [mel_to_hz(m) for m in mel]
+    fp[0] = max(20, fp[0])
+    fp[-1] = min(20000, fp[-1])
+    bands = []
+    for i in range(num_bars):
+        if i >= len(fp) - 1:
+            break
+        s, e = int(fp[i] / width), int(fp[i + 1] / width)
+        if e <= s:
+            e = s + 1
+        s = max(0, min(s, fft_size // 2))
+        e = max(s + 1, min(e, fft_size // 2 + 1))
+        bands.append((s, e))
+    return bands
+
+
+def mel_compensation(fs: float, fft_size: int) -> np.ndarray:
+    """freq_mapper.py:146-163 over np.arange(N/2+1) * fs/N (:57-58)."""
+    f = np.arange(fft_size // 2 + 1) * (fs / fft_size)
+    c = np.ones_like(f)
+    for i, fr in enumerate(f):
+        if fr > 0:
+            if fr < 100:
+                c[i] = 1.0 + (100 - fr) / 100 * 0.5
+            elif fr < 1000:
+                c[i] = 1.0
+            elif fr < 4000:
+                c[i] = 1.0 + (fr - 1000) / 3000 * 0.3
+            else:
+                c[i] = 1.3 - (fr - 4000) / 16000 * 0.5
+    return c
+
+
+def map_spectrum_to_bars(spec: np.ndarray, bands, comp: np.ndarray, num_bars: int,
+                         apply_compensation: bool = True) -> np.ndarray:
+    """freq_mapper.py:165-196: optional per-bin compensation when lengths match, then the band
+    mean; stops at the first band whose end runs past the spectrum."""
+    out = np.zeros(num_bars, np.float32)
+    if apply_compensation and len(spec) == len(comp):
+        spec = spec * comp
+    for i, (s, e) in enumerate(bands):
+        if i >= num_bars or e > len(spec):
+            break
+        out[i] = np.mean(spec[s:e]) if e > s else (spec[s] if s < len(spec) else 0)
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# A12: chromagram binning   (omega4/panels/chromagram.py:109-237; genre 'pop', offset 0)
+# ----------------------------------------------------------------------------------------------
+
+_GENRE_BLEND = {"metal": 0.7, "rock": 0.7, "jazz": 0.5}
+
+
+def suppress_harmonics(fft: np.ndarray, freqs: np.ndarray) -> np.ndarray:
+    """chromagram.py:161-189: strict local maxima above 0.1*max; for h = 2..5 scale the bin closest
+    to h*f (first on ties) by 1/h when it is within 10 Hz."""
+    enh = fft.copy()
+    thr = np.max(fft) * 0.1
+    peaks = [i for i in range(1, len(fft) - 1)
+             if fft[i] > fft[i - 1] and fft[i] > fft[i + 1] and fft[i] > thr]
+    for p in peaks:
+        if p < len(freqs):
+            f0 = freqs[p]
+            for h in range(2, 6):
+                hf = f0 * h
+                c = int(np.argmin(np.abs(freqs - hf)))
+                if c < len(enh) and abs(freqs[c] - hf) < 10:
+                    enh[c] *= 1.0 / h
+    return enh
+
+
+def spectral_weight(f):
+    """chromagram.py:191-201."""
+    return np.where(f < 100, 0.5, np.where(f < 1000, 1.0, np.where(f < 4000, 0.8, 0.6)))
+
+
+def chroma_matrix(freqs: np.ndarray, offset: float = 0.0) -> np.ndarray:
+    """The constant 12 x K projection of chromagram.py:122-146 (Gaussian over 5 neighbours times the
+    spectral weight) for bins with 20 < f < 8000."""
+    M = np.zeros((12, len(freqs)))
+    sel = np.where((freqs > 20) & (freqs < 8000))[0]
+    f = freqs[sel]
+    c = (69 + 12 * np.log2(f / 440.0) + offset) % 12
+    base = np.floor(c).astype(int)  # int() of a non-negative float
+    sw = spectral_weight(f)
+    for o in range(-2, 3):
+        tgt = (base + o) % 12
+        d = np.abs(c - (base + o))
+        w = np.exp(-0.5 * (d / 0.5) ** 2) * sw
+        np.add.at(M, (tgt, sel), w)
+    return M
+
+
+class ChromaState:
+    """Per-stream chroma_history (chromagram.py:96) with the genre blend (:215-237)."""
+
+    def __init__(self, genre: str = "pop"):
+        self.hist = deque(maxlen=8)
+        self.genre = genre
+
+    def compute(self, fft: np.ndarray, freqs: np.ndarray) -> np.ndarray:
+        enh = suppress_harmonics(np.asarray(fft).copy(), freqs)
+        chroma = chroma_matrix(freqs) @ enh.astype(np.float64)
+        sm = np.array([0.25 * chroma[(i - 1) % 12] + 0.5 * chroma[i] + 0.25 * chroma[(i + 1) % 12]
+                       for i in range(12)])
+        if np.sum(sm) > 0:
+            sm = sm / np.sum(sm)
+        self.hist.append(sm.copy())
+        if len(self.hist) == 1:
+            return self.hist[-1]
+        a = _GENRE_BLEND.get(self.genre.lower(), 0.3)
+        return self.hist[-2] * (1 - a) + self.hist[-1] * a
+
+
+# ----------------------------------------------------------------------------------------------
+# A13: BatchedFFTProcessor CPU branch   (omega4/optimization/batched_fft_processor.py:119-146,
+#      :269-285)
+# ----------------------------------------------------------------------------------------------
+
+
+def batched_fft(audio: np.ndarray, fft_size: int, window_type: str = "hann", fs: float = 48000):
+    """prepare_batch pads/trims to fft_size (:136-139), then window * data, np.fft.rfft, abs;
+    frequencies are hard-coded for 48 kHz in the reference (:257)."""
+    a = np.asarray(audio)
+    if len(a) > fft_size:
+        a = a[-fft_size:]
+    elif len(a) < fft_size:
+        a = np.pad(a, (0, fft_size - len(a)))
+    c = np.fft.rfft(a * window_f32(fft_size, window_type))
+    return {"magnitude": np.abs(c), "complex": c, "frequencies": np.fft.rfftfreq(fft_size, 1 / 48000)}
+
+
+# ----------------------------------------------------------------------------------------------
+# One BASELINE cfg2 channel-frame, chained as SURVEY.md §8(c)
+# ----------------------------------------------------------------------------------------------
+
+
+def full_frame(x: np.ndarray, configs=NORTHSTAR_CONFIGS, fs=48000, target_bins=512):
+    """MRFFT + combine(T) + LUFS_inst + TP for one channel-frame (the per-frame part of cfg2)."""
+    res = mrfft_frame(x, configs, fs)
+    comb, _ = combine(res, configs, fs, 20000, target_bins)
+    return res, comb, lufs_instant(x, fs), true_peak(x)

@@ -1,0 +1,179 @@
+"""Pin the oracle: the numpy restatement must reproduce the reference's own outputs (golden vectors
+made by oracle/gen_golden.py from /root/reference) before it is trusted as the GPU checker."""
+import numpy as np
+import pytest
+
+from conftest import load_golden, normwise
+from oracle import omega_ref as R
+from oracle import signals as S
+
+FS = 48000
+
+
+@pytest.fixture(scope="module")
+def mr():
+    return load_golden("mrfft")
+
+
+@pytest.fixture(scope="module")
+def me():
+    return load_golden("meters")
+
+
+def test_fixture_versions(mr):
+    assert list(mr["versions"]) == ["2.2.6", "1.15.3"]
+
+
+@pytest.mark.parametrize("name", ["sine1k_2048", "noise_2048", "triad_4096", "comp_4096",
+                                  "silence_4096", "sine50_8192"])
+def test_mrfft_default(mr, name):
+    x = mr[f"{name}/x"]
+    res = R.mrfft_frame(x, R.DEFAULT_CONFIGS, FS)
+    assert sorted(res) == list(mr[f"{name}/res"])
+    for i in res:
+        np.testing.assert_allclose(res[i], mr[f"{name}/mag{i}"], rtol=0, atol=0)
+        assert res[i].dtype == np.float32
+    raw = R.mrfft_frame(x, R.DEFAULT_CONFIGS, FS, apply_weighting=False)
+    for i in raw:
+        np.testing.assert_array_equal(raw[i], mr[f"{name}/raw{i}"])
+    for T in (512, 1024):
+        c, t = R.combine(res, R.DEFAULT_CONFIGS, FS, 20000, T)
+        np.testing.assert_allclose(c, mr[f"{name}/comb{T}"], rtol=1e-6, atol=1e-7)
+        np.testing.assert_array_equal(t, mr[f"{name}/tgt{T}"])
+
+
+@pytest.mark.parametrize("k", [0, 1, 2])
+def test_mrfft_northstar(mr, k):
+    x = mr[f"ns{k}/x"]
+    res = R.mrfft_frame(x, R.NORTHSTAR_CONFIGS, FS)
+    for i in range(4):
+        np.testing.assert_array_equal(res[i], mr[f"ns{k}/mag{i}"])
+    c, _ = R.combine(res, R.NORTHSTAR_CONFIGS, FS, 20000, 512)
+    np.testing.assert_allclose(c, mr[f"ns{k}/comb512"], rtol=1e-6, atol=1e-7)
+
+
+def test_mrfft_stream(mr):
+    x = mr["stream/x"]
+    st = R.MRFFTStream(R.DEFAULT_CONFIGS, FS)
+    for c in range(24):
+        r = st.process(x[c * 512:(c + 1) * 512])
+        assert sum(1 << i for i in r) == mr["stream/resmask"][c]
+        comb = R.combine(r, R.DEFAULT_CONFIGS, FS, 20000, 512)[0] if r else np.zeros(512)
+        np.testing.assert_allclose(comb, mr["stream/comb512"][c], rtol=1e-6, atol=1e-7)
+    for i in r:
+        np.testing.assert_array_equal(r[i], mr[f"stream/mag{i}"])
+
+
+def test_combine_plan_matches_combine(mr):
+    """The host-side interpolation plan the HIP epilogue uses reproduces combine()."""
+    x = mr["ns0/x"]
+    res = R.mrfft_frame(x, R.NORTHSTAR_CONFIGS, FS)
+    plan = R.combine_table(R.NORTHSTAR_CONFIGS, FS, 20000, 512)
+    out = np.zeros(512)
+    for t, entries in enumerate(plan):
+        acc = ws = 0.0
+        for (i, j, fr) in entries:
+            m = res[i].astype(np.float64)
+            v = m[j] if fr == 0.0 else m[j] + fr * (m[j + 1] - m[j])
+            w = R.NORTHSTAR_CONFIGS[i].weight
+            acc += v * w
+            ws += w
+        out[t] = acc / ws if ws > 0 else 0.0
+    assert normwise(out, mr["ns0/comb512"]) < 1e-6
+
+
+def test_k_weighting_coeffs(me):
+    hp_b, hp_a, sh_b, sh_a = R.k_weighting_coeffs(FS)
+    np.testing.assert_array_equal(hp_b, me["coef/hp_b"])
+    np.testing.assert_array_equal(hp_a, me["coef/hp_a"])
+    np.testing.assert_array_equal(sh_b, me["coef/sh_b"])
+    np.testing.assert_array_equal(sh_a, me["coef/sh_a"])
+
+
+@pytest.mark.parametrize("name", ["comp4800", "square480", "sine2048", "hann2048_f64"])
+def test_k_weighting_signal(me, name):
+    y = R.apply_k_weighting(me[f"kw/{name}/x"], FS)
+    np.testing.assert_allclose(y, me[f"kw/{name}/y"], rtol=1e-12, atol=1e-14)
+    assert abs(R.true_peak(me[f"kw/{name}/x"]) - me[f"kw/{name}/tp"]) < 1e-5
+
+
+def test_filtfilt_restatement_matches_scipy():
+    import scipy.signal as ss
+    x = S.noise(3, 3000, 0.3).astype(np.float64)
+    for b, a in (R.k_weighting_coeffs(FS)[:2], R.k_weighting_coeffs(FS)[2:]):
+        np.testing.assert_allclose(R.filtfilt(b, a, x), ss.filtfilt(b, a, x), rtol=1e-13, atol=1e-15)
+        np.testing.assert_allclose(R.lfilter_zi2(b, a), ss.lfilter_zi(b, a), rtol=1e-10)  # 1+a1+a2 ~ 2.5e-5: ill-conditioned
+
+
+def test_resample_restatement_matches_scipy():
+    import scipy.signal as ss
+    for n in (480, 1024, 4800):
+        x = S.noise(n, n, 0.5)
+        np.testing.assert_allclose(R.resample_fft(x, 4 * n), ss.resample(x, 4 * n), rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("name", ["cfg2L", "sine2048", "low50_4096", "silence", "steps1024", "square1024"])
+def test_meter_sequences(me, name):
+    li, tp, agg = R.meter_sequence(me[f"{name}/x"], FS)
+    np.testing.assert_allclose(li, me[f"{name}/lufs_inst"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(tp, me[f"{name}/tp"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(agg, me[f"{name}/agg"], rtol=0, atol=1e-5)
+
+
+def test_meter_long_window(me):
+    """3700 frames: the 3600-deep integrated deque evicts (professional_meters.py:22)."""
+    li, tp, agg = R.meter_sequence(S.level_steps(3700, 512, seed=9), FS)
+    np.testing.assert_allclose(li, me["long/lufs_inst"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(agg, me["long/agg"], rtol=0, atol=1e-5)
+
+
+def test_known_answers(me):
+    li, tp, agg = R.meter_sequence(np.zeros((3, 2048), np.float32), FS)
+    assert (li == -100).all() and (tp == -100).all()
+    assert agg[-1].tolist() == [-100.0, -100.0, -100.0, 0.0, -100.0]
+
+
+def test_bands(golden):
+    g = golden("bands")
+    mags = g["mags8192"]
+    for nb, fft in ((512, 8192), (768, 4096)):
+        s, e, c = R.pipeline_band_table(FS, nb, fft)
+        np.testing.assert_array_equal(s, g[f"pipe{nb}_{fft}/starts"])
+        np.testing.assert_array_equal(e, g[f"pipe{nb}_{fft}/ends"])
+        np.testing.assert_array_equal(c, g[f"pipe{nb}_{fft}/comp"])
+        src = mags if fft == 8192 else mags[:, : fft // 2 + 1]
+        out = np.stack([R.map_to_bands(m, s, e, c, nb) for m in src])
+        np.testing.assert_array_equal(out, g[f"pipe{nb}_{fft}/out"])
+        st = np.zeros(nb, np.float32)
+        sm = np.stack([R.map_to_bands(m, s, e, c, nb, st) for m in src])
+        np.testing.assert_allclose(sm, g[f"pipe{nb}_{fft}/smooth"], rtol=1e-6)
+        assert out[:, -1].max() == 0  # only B-1 bands are produced
+    for fft, nb in ((2048, 512), (8192, 512)):
+        bands = R.mel_band_table(FS, fft, nb)
+        np.testing.assert_array_equal(np.array(bands), g[f"mel{fft}_{nb}/bands"])
+        comp = R.mel_compensation(FS, fft)
+        np.testing.assert_array_equal(comp, g[f"mel{fft}_{nb}/comp"])
+        spec = g[f"mel{fft}_{nb}/spec"]
+        for key, fn in (("out_comp", lambda s: R.map_spectrum_to_bars(s, bands, comp, nb, True)),
+                        ("out_raw", lambda s: R.map_spectrum_to_bars(s, bands, comp, nb, False)),
+                        ("out_512in", lambda s: R.map_spectrum_to_bars(s[:512], bands, comp, nb, False))):
+            np.testing.assert_allclose(np.stack([fn(s) for s in spec]), g[f"mel{fft}_{nb}/{key}"], rtol=1e-6)
+
+
+def test_chroma(golden):
+    g = golden("chroma")
+    st = R.ChromaState()
+    out = np.stack([st.compute(m, g["freqs"]) for m in g["mags"]])
+    np.testing.assert_allclose(out, g["out"], rtol=1e-10, atol=1e-14)
+    a = R.ChromaState().compute(g["a440_mag"], g["freqs"])
+    np.testing.assert_allclose(a, g["a440_out"], rtol=1e-10)
+    assert int(np.argmax(a)) == 9  # A
+
+
+def test_batched(golden):
+    g = golden("batched")
+    for name, n, w in (("app_f64_2048_hann", 2048, "hann"), ("f32_4096_blackman", 4096, "blackman"),
+                       ("pad_1000_1024_hamming", 1024, "hamming"), ("trim_20000_16384_hann", 16384, "hann")):
+        r = R.batched_fft(g[f"{name}/x"], n, w)
+        np.testing.assert_array_equal(r["magnitude"], g[f"{name}/mag"])
+        np.testing.assert_array_equal(r["complex"], g[f"{name}/complex"])
