@@ -1,0 +1,1004 @@
+// libomega.so host side: the C ABI declared in include/omega.h.
+//
+// The context precomputes (in float64, cast like the reference casts) every table the kernels read:
+// windows (np.blackman/np.hanning/np.hamming), psychoacoustic weights (multi_resolution_fft.py:304-329,
+// float32 compounding), the combine plan (multi_resolution_fft.py:353-395), FFT twiddles, the
+// true-peak rotation table, the two K-weighting biquads in state-space form with their chunk-scan
+// tables (professional_meters.py:48-72, scipy.signal.butter/lfilter_zi closed forms), and owns the
+// per-channel meter state (professional_meters.py:19-25) on the device, double-buffered.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/omega.h"
+#include "params.hpp"
+
+namespace omega {
+hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s);
+hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
+hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
+hipError_t launch_meters(const MeterParams& p, const MeterStateParams& sp, hipStream_t s);
+hipError_t launch_bands(const BandParams& p, hipStream_t s);
+hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int hi, const double* mat, double* out,
+                         hipStream_t s);
+hipError_t launch_combine(const CombineParams& p, hipStream_t s);
+}  // namespace omega
+
+using namespace omega;
+
+namespace {
+
+constexpr double kPi = 3.14159265358979323846;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+};
+
+bool is_pow2_in(int v, int lo, int hi) { return v >= lo && v <= hi && (v & (v - 1)) == 0; }
+
+// numpy window formulas (numpy 2.x): n = arange(1-M, M, 2)
+std::vector<float> make_window(int M, int kind) {
+  std::vector<float> w(M);
+  for (int i = 0; i < M; ++i) {
+    const double n = (double)(1 - M + 2 * i);
+    double v;
+    switch (kind) {
+      case OMEGA_WIN_BLACKMAN: v = 0.42 + 0.5 * std::cos(kPi * n / (M - 1)) + 0.08 * std::cos(2.0 * kPi * n / (M - 1)); break;
+      case OMEGA_WIN_HANN: v = 0.5 + 0.5 * std::cos(kPi * n / (M - 1)); break;
+      case OMEGA_WIN_HAMMING: v = 0.54 + 0.46 * std::cos(kPi * n / (M - 1)); break;
+      default: v = 1.0;
+    }
+    if (M == 1) v = 1.0;
+    w[i] = (float)v;
+  }
+  return w;
+}
+
+// np.fft.rfftfreq(N, 1/fs)
+double rfreq(int k, int N, double fs) {
+  const double d = 1.0 / fs;
+  const double val = 1.0 / (N * d);
+  return k * val;
+}
+
+struct BiquadCoef {
+  double b[3], a[3];
+};
+
+// scipy.signal.butter(2, fc/(fs/2), 'high') (bilinear transform, prewarped)
+BiquadCoef butter2_highpass(double fc, double fs) {
+  const double K = std::tan(kPi * fc / fs);
+  const double n = 1.0 + std::sqrt(2.0) * K + K * K;
+  BiquadCoef c;
+  c.b[0] = 1.0 / n;
+  c.b[1] = -2.0 / n;
+  c.b[2] = 1.0 / n;
+  c.a[0] = 1.0;
+  c.a[1] = 2.0 * (K * K - 1.0) / n;
+  c.a[2] = (1.0 - std::sqrt(2.0) * K + K * K) / n;
+  return c;
+}
+
+void mat2_mul(const double* A, const double* B, double* C) {
+  double t[4] = {A[0] * B[0] + A[1] * B[2], A[0] * B[1] + A[1] * B[3], A[2] * B[0] + A[3] * B[2],
+                 A[2] * B[1] + A[3] * B[3]};
+  std::memcpy(C, t, sizeof t);
+}
+
+BiquadTab make_biquad_tab(const BiquadCoef& c, int L) {
+  BiquadTab t{};
+  const double b0 = c.b[0], a1 = c.a[1], a2 = c.a[2];
+  const double B0 = c.b[1] - a1 * b0, B1 = c.b[2] - a2 * b0;
+  t.b0 = (float)b0;
+  t.a1 = (float)a1;
+  t.a2 = (float)a2;
+  t.B0 = (float)B0;
+  t.B1 = (float)B1;
+  // scipy.signal.lfilter_zi: solve (I - companion(a).T) zi = B
+  const double z0 = (B0 + B1) / (1.0 + a1 + a2);
+  t.zi0 = (float)z0;
+  t.zi1 = (float)(B1 - a2 * z0);
+  const double A[4] = {-a1, 1.0, -a2, 0.0};
+  double An[4] = {1, 0, 0, 1};
+  for (int n = 0; n < 64; ++n) {
+    if (n < L) {
+      t.h0[n] = (float)An[0];
+      t.h1[n] = (float)An[1];
+    }
+    if (n + 1 <= L) mat2_mul(A, An, An);
+  }
+  // An = A^L now (L <= 64)
+  double P[4];
+  std::memcpy(P, An, sizeof P);
+  double Pk[4] = {P[0], P[1], P[2], P[3]};
+  for (int l = 0; l < 64; ++l) {
+    for (int q = 0; q < 4; ++q) t.pw[l][q] = (float)Pk[q];
+    mat2_mul(P, Pk, Pk);
+  }
+  return t;
+}
+
+}  // namespace
+
+struct omega_bands {
+  omega_ctx* ctx;
+  int op, n_bands, n_out, n_bins, n_valid;
+  int32_t* d_starts;
+  int32_t* d_ends;
+  float* d_scale;
+  float* d_bin_scale;
+};
+
+struct omega_ctx {
+  omega_config cfg{};
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  std::string err;
+  // tables
+  float2* d_tw[kMaxLog2] = {};
+  float2* d_rot = nullptr;
+  float* d_win[kMaxRes] = {};
+  float* d_wgt[kMaxRes] = {};
+  int* d_ent_t = nullptr;
+  int* d_ent_j = nullptr;
+  float* d_ent_frac = nullptr;
+  float* d_wsum = nullptr;
+  int ent_begin[kMaxRes] = {}, ent_end[kMaxRes] = {};
+  std::map<int, BiquadTab*> kw_tabs;  // M -> device {hp, shelf}
+  std::map<std::pair<int, int>, float*> windows;  // (m, kind) -> device window
+  std::map<int, float2*> rots;                     // m -> true-peak rotation table
+  // combine plan as per-target owner lists (CSR) for omega_combine over a subset of resolutions
+  int* d_own_off = nullptr;
+  int* d_own_rj = nullptr;  // (r << 24) | j
+  float* d_own_frac = nullptr;
+  std::map<int, std::pair<double*, std::pair<int, int>>> chroma_mats;  // n_bins -> (mat, [lo, hi))
+  double chroma_df = 0.0;
+  // meter state (double-buffered)
+  float* d_hist_l[2] = {};
+  float* d_hist_t[2] = {};
+  int* d_nl[2] = {};
+  int* d_nt[2] = {};
+  int cur = 0;
+  int HL = 0, HT = 0;
+  // staging for OMEGA_MEM_HOST
+  std::vector<DevBuf> stage;
+  std::vector<void*> allocs;
+};
+
+namespace {
+
+int fail(omega_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPC(ctx, x)                                                                           \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) return fail(ctx, OMEGA_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+int dalloc(omega_ctx* c, T** p, size_t count) {
+  void* q = nullptr;
+  const hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+  if (e != hipSuccess) return fail(c, OMEGA_ENOMEM, "hipMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
+  c->allocs.push_back(q);
+  *p = static_cast<T*>(q);
+  return 0;
+}
+
+template <class T>
+int upload(omega_ctx* c, T** p, const std::vector<T>& v) {
+  int r = dalloc(c, p, v.size());
+  if (r) return r;
+  HIPC(c, hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+
+// staging buffer slot i of at least bytes
+int stage_buf(omega_ctx* c, int i, size_t bytes, void** out) {
+  if ((int)c->stage.size() <= i) c->stage.resize(i + 1);
+  DevBuf& b = c->stage[i];
+  if (b.n < bytes) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    const hipError_t e = hipMalloc(&b.p, std::max<size_t>(bytes, 256));
+    if (e != hipSuccess) return fail(c, OMEGA_ENOMEM, "staging hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    b.n = std::max<size_t>(bytes, 256);
+  }
+  *out = b.p;
+  return 0;
+}
+
+int build_twiddles(omega_ctx* c) {
+  for (int l = 1; l < kMaxLog2; ++l) {
+    const int N = 1 << l;
+    std::vector<float2> t(N);
+    for (int m = 0; m < N; ++m) {
+      const double a = 2.0 * kPi * (double)m / (double)N;
+      t[m] = make_float2((float)std::cos(a), (float)-std::sin(a));
+    }
+    int r = upload(c, &c->d_tw[l], t);
+    if (r) return r;
+  }
+  return 0;
+}
+
+int get_kw_tab(omega_ctx* c, int M, BiquadTab** out) {
+  auto it = c->kw_tabs.find(M);
+  if (it != c->kw_tabs.end()) {
+    *out = it->second;
+    return 0;
+  }
+  const double fs = c->cfg.sample_rate;
+  const int L = M / 256;
+  std::vector<BiquadTab> t = {make_biquad_tab(butter2_highpass(38.0, fs), L),
+                              make_biquad_tab(butter2_highpass(1500.0, fs), L)};
+  BiquadTab* d = nullptr;
+  int r = upload(c, &d, t);
+  if (r) return r;
+  c->kw_tabs[M] = d;
+  *out = d;
+  return 0;
+}
+
+int get_window(omega_ctx* c, int m, int kind, float** out) {
+  auto key = std::make_pair(m, kind);
+  auto it = c->windows.find(key);
+  if (it != c->windows.end()) {
+    *out = it->second;
+    return 0;
+  }
+  float* d = nullptr;
+  int r = upload(c, &d, make_window(m, kind));
+  if (r) return r;
+  c->windows[key] = d;
+  *out = d;
+  return 0;
+}
+
+// true-peak rotation e^{2 pi i k / (4M)}, k <= M/2
+int get_rot(omega_ctx* c, int M, float2** out) {
+  auto it = c->rots.find(M);
+  if (it != c->rots.end()) {
+    *out = it->second;
+    return 0;
+  }
+  std::vector<float2> rot(M / 2 + 1);
+  for (int k = 0; k <= M / 2; ++k) {
+    const double a = 2.0 * kPi * (double)k / (4.0 * M);
+    rot[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  float2* d = nullptr;
+  int r = upload(c, &d, rot);
+  if (r) return r;
+  c->rots[M] = d;
+  *out = d;
+  return 0;
+}
+
+int validate(omega_ctx* c, const omega_config* cfg) {
+  // MultiResolutionFFT.__init__ (multi_resolution_fft.py:139-142) and FFTConfig.__post_init__ (:35-44)
+  if (cfg->sample_rate <= 0) return fail(c, OMEGA_EINVAL, "Sample rate must be positive");
+  if (cfg->max_freq <= 0 || cfg->max_freq > cfg->sample_rate / 2.0)
+    return fail(c, OMEGA_EINVAL, "Max frequency must be positive and <= Nyquist");
+  if (cfg->n_res < 1 || cfg->n_res > OMEGA_MAX_RES) return fail(c, OMEGA_EINVAL, "n_res must be 1..%d", OMEGA_MAX_RES);
+  for (int r = 0; r < cfg->n_res; ++r) {
+    const omega_resolution& q = cfg->res[r];
+    if (q.freq_lo >= q.freq_hi) return fail(c, OMEGA_EINVAL, "Invalid frequency range: (%g, %g)", q.freq_lo, q.freq_hi);
+    if (q.fft_size <= 0 || (q.fft_size & (q.fft_size - 1)) != 0)
+      return fail(c, OMEGA_EINVAL, "FFT size must be power of 2: %d", q.fft_size);
+    if (q.hop_size <= 0) return fail(c, OMEGA_EINVAL, "Hop size must be positive: %d", q.hop_size);
+    if (!(q.weight > 0)) return fail(c, OMEGA_EINVAL, "Weight must be positive: %g", q.weight);
+  }
+  if (!is_pow2_in(cfg->frame_size, 512, 16384))
+    return fail(c, OMEGA_EUNSUP, "frame_size %d: power of two 512..16384 required", cfg->frame_size);
+  for (int r = 0; r < cfg->n_res; ++r) {
+    const omega_resolution& q = cfg->res[r];
+    if (q.fft_size < 512 || q.fft_size > cfg->frame_size)
+      return fail(c, OMEGA_EUNSUP, "fft_size %d: 512..frame_size(%d) supported", q.fft_size, cfg->frame_size);
+  }
+  if (cfg->target_bins < 1 || cfg->target_bins > (1 << 24)) return fail(c, OMEGA_EINVAL, "target_bins out of range");
+  if (cfg->n_channels < 1) return fail(c, OMEGA_EINVAL, "n_channels must be >= 1");
+  if (cfg->integrated_len < 1 || cfg->integrated_len > 57 * 64)
+    return fail(c, OMEGA_EUNSUP, "integrated_len %d: 1..3648 supported", cfg->integrated_len);
+  if (cfg->momentary_len < 1 || cfg->short_len < 1 || cfg->peak_len < 1)
+    return fail(c, OMEGA_EINVAL, "deque lengths must be >= 1");
+  return 0;
+}
+
+int build_spectral_tables(omega_ctx* c) {
+  const omega_config& cfg = c->cfg;
+  const double fs = cfg.sample_rate;
+  for (int r = 0; r < cfg.n_res; ++r) {
+    const omega_resolution& q = cfg.res[r];
+    const int N = q.fft_size;
+    int e = get_window(c, N, q.window, &c->d_win[r]);
+    if (e) return e;
+    // multi_resolution_fft.py:310-326 -- float32 weights, float32 compounding
+    std::vector<float> w(N / 2 + 1);
+    for (int k = 0; k <= N / 2; ++k) {
+      const double f = rfreq(k, N, fs);
+      float v = (float)q.weight;
+      if (cfg.apply_weighting) {
+        const bool in = f >= q.freq_lo && f <= q.freq_hi;
+        if (in && f >= 60 && f <= 120) v = v * 1.8f;
+        if (in && f >= 200 && f <= 400) v = v * 1.4f;
+        if (in && f >= 2000 && f <= 5000) v = v * 1.2f;
+        if (in && f >= 20 && f <= 80) v = v * 1.6f;
+      } else {
+        v = 1.0f;
+      }
+      w[k] = v;
+    }
+    e = upload(c, &c->d_wgt[r], w);
+    if (e) return e;
+  }
+  // combine plan (multi_resolution_fft.py:353-395)
+  const int T = cfg.target_bins;
+  const double mf = std::min(cfg.max_freq, fs / 2);
+  std::vector<double> tgt(T);
+  const double step = T > 1 ? mf / (T - 1) : 0.0;  // np.linspace(0, mf, T)
+  for (int t = 0; t < T; ++t) tgt[t] = t * step;
+  if (T > 1) tgt[T - 1] = mf;
+  struct Ent {
+    int r, j;
+    float fr;
+  };
+  std::vector<std::vector<Ent>> own(T);
+  for (int r = 0; r < cfg.n_res; ++r) {
+    const omega_resolution& q = cfg.res[r];
+    const int N = q.fft_size;
+    std::vector<int> vidx;
+    for (int k = 0; k <= N / 2; ++k) {
+      const double f = rfreq(k, N, fs);
+      if (f >= q.freq_lo && f <= q.freq_hi) vidx.push_back(k);
+    }
+    if (vidx.size() < 2) continue;  // :367-374
+    for (int t = 0; t < T; ++t) {
+      const double x = tgt[t];
+      if (!(x >= q.freq_lo && x <= q.freq_hi)) continue;
+      const double f0 = rfreq(vidx.front(), N, fs), f1 = rfreq(vidx.back(), N, fs);
+      Ent en{r, 0, 0.f};
+      if (x <= f0) {
+        en.j = vidx.front();
+      } else if (x >= f1) {
+        en.j = vidx.back();
+      } else {
+        // vidx is contiguous: x in [f_j, f_{j+1})
+        const double val = rfreq(1, N, fs);
+        int j = (int)std::floor(x / val);
+        j = std::max(vidx.front(), std::min(j, vidx.back() - 1));
+        while (j > vidx.front() && rfreq(j, N, fs) > x) --j;
+        while (j + 1 < vidx.back() && rfreq(j + 1, N, fs) <= x) ++j;
+        const double fa = rfreq(j, N, fs), fb = rfreq(j + 1, N, fs);
+        en.j = j;
+        en.fr = (float)((x - fa) / (fb - fa));
+      }
+      own[t].push_back(en);
+    }
+  }
+  std::vector<std::vector<int>> et(cfg.n_res), ej(cfg.n_res);
+  std::vector<std::vector<float>> ef(cfg.n_res);
+  std::vector<float> wsum(T, 0.f);
+  int first_res = -1;
+  for (int r = 0; r < cfg.n_res; ++r)
+    if (first_res < 0) first_res = r;
+  for (int t = 0; t < T; ++t) {
+    const auto& o = own[t];
+    for (const Ent& en : o) wsum[t] += (float)cfg.res[en.r].weight;
+    if (o.empty()) {
+      et[first_res].push_back(t | (4 << 24));
+      ej[first_res].push_back(0);
+      ef[first_res].push_back(0.f);
+      continue;
+    }
+    for (size_t q = 0; q < o.size(); ++q) {
+      int mode = o.size() == 1 ? 0 : (q == 0 ? 1 : (q + 1 == o.size() ? 3 : 2));
+      et[o[q].r].push_back(t | (mode << 24));
+      ej[o[q].r].push_back(o[q].j);
+      ef[o[q].r].push_back(o[q].fr);
+    }
+  }
+  std::vector<int> at, aj;
+  std::vector<float> af;
+  for (int r = 0; r < cfg.n_res; ++r) {
+    c->ent_begin[r] = (int)at.size();
+    at.insert(at.end(), et[r].begin(), et[r].end());
+    aj.insert(aj.end(), ej[r].begin(), ej[r].end());
+    af.insert(af.end(), ef[r].begin(), ef[r].end());
+    c->ent_end[r] = (int)at.size();
+  }
+  std::vector<int> ooff(1, 0), orj;
+  std::vector<float> ofr;
+  for (int t = 0; t < T; ++t) {
+    for (const Ent& en : own[t]) {
+      orj.push_back((en.r << 24) | en.j);
+      ofr.push_back(en.fr);
+    }
+    ooff.push_back((int)orj.size());
+  }
+  int e = upload(c, &c->d_own_off, ooff);
+  if (!e) e = upload(c, &c->d_own_rj, orj);
+  if (!e) e = upload(c, &c->d_own_frac, ofr);
+  if (!e) e = upload(c, &c->d_ent_t, at);
+  if (!e) e = upload(c, &c->d_ent_j, aj);
+  if (!e) e = upload(c, &c->d_ent_frac, af);
+  if (!e) e = upload(c, &c->d_wsum, wsum);
+  if (e) return e;
+  return get_rot(c, cfg.frame_size, &c->d_rot);
+}
+
+int build_meter_state(omega_ctx* c) {
+  const int C = c->cfg.n_channels;
+  c->HL = std::max(1, c->cfg.integrated_len - 1);
+  c->HT = std::max(1, c->cfg.peak_len - 1);
+  for (int b = 0; b < 2; ++b) {
+    int e = dalloc(c, &c->d_hist_l[b], (size_t)C * c->HL);
+    if (!e) e = dalloc(c, &c->d_hist_t[b], (size_t)C * c->HT);
+    if (!e) e = dalloc(c, &c->d_nl[b], C);
+    if (!e) e = dalloc(c, &c->d_nt[b], C);
+    if (e) return e;
+  }
+  return omega_meter_reset(c);
+}
+
+SpectralParams spectral_params(omega_ctx* c) {
+  SpectralParams p{};
+  p.C = c->cfg.n_channels;
+  p.n_res = c->cfg.n_res;
+  for (int r = 0; r < p.n_res; ++r) {
+    ResParam& q = p.res[r];
+    q.n = c->cfg.res[r].fft_size;
+    q.offset = c->cfg.frame_size - q.n;
+    q.win = c->d_win[r];
+    q.wgt = c->d_wgt[r];
+    q.ent_begin = c->ent_begin[r];
+    q.ent_end = c->ent_end[r];
+    q.cw = (float)c->cfg.res[r].weight;
+  }
+  p.ent_t = c->d_ent_t;
+  p.ent_j = c->d_ent_j;
+  p.ent_frac = c->d_ent_frac;
+  p.wsum = c->d_wsum;
+  p.T = c->cfg.target_bins;
+  p.rot = c->d_rot;
+  for (int l = 0; l < kMaxLog2; ++l) p.tw[l] = c->d_tw[l];
+  return p;
+}
+
+bool aligned8(const void* p) { return ((uintptr_t)p & 7) == 0; }
+
+// ---- host-memory staging helpers ----
+struct HostOut {
+  void* host;
+  void* dev;
+  size_t bytes;
+};
+
+int stage_in(omega_ctx* c, int slot, const void* host, size_t bytes, const void** dev) {
+  void* d = nullptr;
+  int e = stage_buf(c, slot, bytes, &d);
+  if (e) return e;
+  HIPC(c, hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, c->stream));
+  *dev = d;
+  return 0;
+}
+
+template <class T>
+int stage_out(omega_ctx* c, int slot, T* host, size_t count, std::vector<HostOut>& outs, T** dev) {
+  if (!host) {
+    *dev = nullptr;
+    return 0;
+  }
+  void* d = nullptr;
+  int e = stage_buf(c, slot, count * sizeof(T), &d);
+  if (e) return e;
+  outs.push_back({host, d, count * sizeof(T)});
+  *dev = static_cast<T*>(d);
+  return 0;
+}
+
+int finish_host(omega_ctx* c, const std::vector<HostOut>& outs) {
+  for (const HostOut& o : outs) HIPC(c, hipMemcpyAsync(o.host, o.dev, o.bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_frames, double* out) {
+  MeterParams p{};
+  p.lufs = lufs;
+  p.tp = tp;
+  p.n_frames = n_frames;
+  p.C = c->cfg.n_channels;
+  p.hist_l = c->d_hist_l[c->cur];
+  p.hist_t = c->d_hist_t[c->cur];
+  p.n_hist_l = c->d_nl[c->cur];
+  p.n_hist_t = c->d_nt[c->cur];
+  p.HL = c->HL;
+  p.HT = c->HT;
+  p.mom_len = c->cfg.momentary_len;
+  p.short_len = c->cfg.short_len;
+  p.int_len = c->cfg.integrated_len;
+  p.peak_len = c->cfg.peak_len;
+  p.gate = (float)c->cfg.gate_lufs;
+  p.out = out;
+  MeterStateParams s{};
+  s.lufs = lufs;
+  s.tp = tp;
+  s.n_frames = n_frames;
+  s.C = p.C;
+  s.hist_l_in = p.hist_l;
+  s.hist_t_in = p.hist_t;
+  s.n_l_in = p.n_hist_l;
+  s.n_t_in = p.n_hist_t;
+  const int nx = c->cur ^ 1;
+  s.hist_l_out = c->d_hist_l[nx];
+  s.hist_t_out = c->d_hist_t[nx];
+  s.n_l_out = c->d_nl[nx];
+  s.n_t_out = c->d_nt[nx];
+  s.HL = c->HL;
+  s.HT = c->HT;
+  HIPC(c, launch_meters(p, s, c->stream));
+  c->cur = nx;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* omega_version(void) { return "omega-mi355x 0.1 (gfx950, ABI 1)"; }
+
+void omega_config_default(omega_config* cfg) {
+  std::memset(cfg, 0, sizeof *cfg);
+  cfg->sample_rate = 48000;
+  cfg->max_freq = 20000;
+  cfg->n_res = 4;
+  const omega_resolution def[4] = {{20, 200, 4096, 1024, 1.5, OMEGA_WIN_BLACKMAN},
+                                   {200, 1000, 2048, 512, 1.2, OMEGA_WIN_BLACKMAN},
+                                   {1000, 5000, 1024, 256, 1.0, OMEGA_WIN_BLACKMAN},
+                                   {5000, 20000, 1024, 256, 1.5, OMEGA_WIN_BLACKMAN}};
+  std::memcpy(cfg->res, def, sizeof def);
+  cfg->apply_weighting = 1;
+  cfg->target_bins = 1024;
+  cfg->frame_size = 4096;
+  cfg->n_channels = 1;
+  cfg->gate_lufs = -70.0;
+  cfg->momentary_len = 24;
+  cfg->short_len = 180;
+  cfg->integrated_len = 3600;
+  cfg->peak_len = 60;
+}
+
+int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
+  if (!cfg || !out) return OMEGA_EINVAL;
+  *out = nullptr;
+  omega_ctx* c = new (std::nothrow) omega_ctx();
+  if (!c) return OMEGA_ENOMEM;
+  int e = validate(c, cfg);
+  if (e) {
+    // surface the message through a throwaway context: callers read it via omega_last_error(*out)
+    *out = c;
+    return e;
+  }
+  c->cfg = *cfg;
+  c->device = device;
+  hipError_t he = hipSetDevice(device);
+  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+  if (he != hipSuccess) {
+    *out = c;
+    return fail(c, OMEGA_EHIP, "device %d: %s", device, hipGetErrorString(he));
+  }
+  c->stream = c->own;
+  e = build_twiddles(c);
+  if (!e) e = build_spectral_tables(c);
+  if (!e) e = build_meter_state(c);
+  *out = c;
+  return e;
+}
+
+void omega_destroy(omega_ctx* c) {
+  if (!c) return;
+  if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->own) (void)hipStreamSynchronize(c->own);
+  for (void* p : c->allocs) (void)hipFree(p);
+  for (auto& kv : c->chroma_mats) (void)hipFree(kv.second.first);
+  for (DevBuf& b : c->stage)
+    if (b.p) (void)hipFree(b.p);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+const char* omega_last_error(const omega_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int omega_set_stream(omega_ctx* c, void* s) {
+  if (!c) return OMEGA_EINVAL;
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own;
+  return 0;
+}
+
+int omega_synchronize(omega_ctx* c) {
+  if (!c) return OMEGA_EINVAL;
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int omega_meter_reset(omega_ctx* c) {
+  if (!c) return OMEGA_EINVAL;
+  const int C = c->cfg.n_channels;
+  for (int b = 0; b < 2; ++b) {
+    HIPC(c, hipMemsetAsync(c->d_nl[b], 0, C * sizeof(int), c->stream));
+    HIPC(c, hipMemsetAsync(c->d_nt[b], 0, C * sizeof(int), c->stream));
+  }
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t frame_stride, int64_t channel_stride,
+                         const omega_outputs* out, int mem) {
+  if (!c || !out) return OMEGA_EINVAL;
+  if (!x || n_frames < 0) return fail(c, OMEGA_EINVAL, "null input or negative frame count");
+  if (n_frames == 0) return 0;
+  const int C = c->cfg.n_channels, W = c->cfg.frame_size, T = c->cfg.target_bins;
+  const int64_t ncf = n_frames * C;
+  if ((frame_stride & 1) || (channel_stride & 1))
+    return fail(c, OMEGA_EINVAL, "frame_stride and channel_stride must be even (8-byte aligned frames)");
+  if (ncf > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "too many channel-frames");
+  HIPC(c, hipSetDevice(c->device));
+  SpectralParams sp = spectral_params(c);
+  sp.frame_stride = frame_stride;
+  sp.chan_stride = channel_stride;
+  sp.n_cf = ncf;
+  std::vector<HostOut> outs;
+  const float* dx = x;
+  float* tp = out->true_peak_db;
+  float* lufs = out->lufs_inst;
+  double* meters = out->meters;
+  float* comb = out->combined;
+  float* weighted = out->weighted;
+  float* mags[kMaxRes] = {};
+  const size_t span = (size_t)((n_frames - 1) * frame_stride + (C - 1) * channel_stride + W);
+  int e = 0;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 0, x, span * sizeof(float), reinterpret_cast<const void**>(&dx));
+    if (!e) e = stage_out(c, 1, comb, ncf * T, outs, &comb);
+    if (!e) e = stage_out(c, 2, out->lufs_inst, ncf, outs, &lufs);
+    if (!e) e = stage_out(c, 3, out->true_peak_db, ncf, outs, &tp);
+    if (!e) e = stage_out(c, 4, out->meters, ncf * 5, outs, &meters);
+    if (!e) e = stage_out(c, 5, out->weighted, ncf * W, outs, &weighted);
+    for (int r = 0; r < c->cfg.n_res && !e; ++r)
+      e = stage_out(c, 6 + r, out->mag[r], ncf * (c->cfg.res[r].fft_size / 2 + 1), outs, &mags[r]);
+    if (e) return e;
+  } else {
+    for (int r = 0; r < c->cfg.n_res; ++r) mags[r] = out->mag[r];
+    if (!aligned8(x)) return fail(c, OMEGA_EINVAL, "input must be 8-byte aligned");
+  }
+  // meters need the instantaneous values even when the caller does not ask for them
+  if (meters && !lufs) {
+    e = stage_buf(c, 10, ncf * sizeof(float), reinterpret_cast<void**>(&lufs));
+    if (e) return e;
+  }
+  if (meters && !tp) {
+    e = stage_buf(c, 11, ncf * sizeof(float), reinterpret_cast<void**>(&tp));
+    if (e) return e;
+  }
+  sp.x = dx;
+  sp.comb_out = comb;
+  sp.tp_out = tp;
+  for (int r = 0; r < c->cfg.n_res; ++r) sp.res[r].mag_out = mags[r];
+  HIPC(c, launch_spectral(W, sp, c->stream));
+  if (lufs || weighted) {
+    BiquadTab* tabs = nullptr;
+    e = get_kw_tab(c, W, &tabs);
+    if (e) return e;
+    KWeightParams kp{dx, frame_stride, channel_stride, C, ncf, tabs, tabs + 1, lufs, weighted, 0};
+    HIPC(c, launch_kweight(W, kp, c->stream));
+  }
+  if (meters) {
+    e = meters_enqueue(c, lufs, tp, n_frames, meters);
+    if (e) return e;
+  }
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+int omega_combine(omega_ctx* c, const float* const* mags, int64_t n_cf, float* out, int mem) {
+  if (!c || !mags || !out) return OMEGA_EINVAL;
+  if (n_cf <= 0) return n_cf == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  HIPC(c, hipSetDevice(c->device));
+  const int T = c->cfg.target_bins;
+  CombineParams p{};
+  std::vector<HostOut> outs;
+  float* dout = out;
+  int e = 0;
+  for (int r = 0; r < c->cfg.n_res; ++r) {
+    p.nbins[r] = c->cfg.res[r].fft_size / 2 + 1;
+    p.cw[r] = (float)c->cfg.res[r].weight;
+    if (!mags[r]) continue;
+    if (mem == OMEGA_MEM_HOST) {
+      const void* d = nullptr;
+      e = stage_in(c, 20 + r, mags[r], (size_t)n_cf * p.nbins[r] * sizeof(float), &d);
+      if (e) return e;
+      p.mag[r] = static_cast<const float*>(d);
+    } else {
+      p.mag[r] = mags[r];
+    }
+  }
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_out(c, 24, out, (size_t)n_cf * T, outs, &dout);
+    if (e) return e;
+  }
+  p.n_cf = n_cf;
+  p.T = T;
+  p.own_off = c->d_own_off;
+  p.own_rj = c->d_own_rj;
+  p.own_frac = c->d_own_frac;
+  p.out = dout;
+  HIPC(c, launch_combine(p, c->stream));
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+int omega_true_peak(omega_ctx* c, const float* x, int64_t n, int32_t m, float* out_db, int mem) {
+  if (!c || !x || !out_db) return OMEGA_EINVAL;
+  if (!is_pow2_in(m, 512, 16384)) return fail(c, OMEGA_EUNSUP, "true peak: frame length %d unsupported", m);
+  if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  HIPC(c, hipSetDevice(c->device));
+  std::vector<HostOut> outs;
+  const float* dx = x;
+  float* dout = out_db;
+  int e = 0;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 0, x, (size_t)n * m * sizeof(float), reinterpret_cast<const void**>(&dx));
+    if (!e) e = stage_out(c, 3, out_db, n, outs, &dout);
+    if (e) return e;
+  }
+  SpectralParams sp = spectral_params(c);
+  sp.x = dx;
+  sp.C = 1;
+  sp.frame_stride = m;
+  sp.chan_stride = 0;
+  sp.n_cf = n;
+  sp.comb_out = nullptr;
+  for (int r = 0; r < kMaxRes; ++r) sp.res[r].mag_out = nullptr;
+  sp.n_res = 0;
+  sp.tp_out = dout;
+  float2* rot = nullptr;
+  e = get_rot(c, m, &rot);
+  if (e) return e;
+  sp.rot = rot;
+  HIPC(c, launch_spectral(m, sp, c->stream));
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+int omega_k_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, float* weighted, float* lufs_inst,
+                      int mem) {
+  return omega_weighting(c, x, n, m, OMEGA_WEIGHT_K, weighted, lufs_inst, mem);
+}
+
+int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t mode, float* weighted,
+                    float* lufs_inst, int mem) {
+  if (!c || !x) return OMEGA_EINVAL;
+  if (mode != OMEGA_WEIGHT_K && mode != OMEGA_WEIGHT_Z)
+    return fail(c, OMEGA_EUNSUP, "weighting mode %d: only K and Z are implemented", mode);
+  if (!is_pow2_in(m, 512, 16384)) return fail(c, OMEGA_EUNSUP, "k-weighting: frame length %d unsupported", m);
+  if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  HIPC(c, hipSetDevice(c->device));
+  std::vector<HostOut> outs;
+  const float* dx = x;
+  float* dw = weighted;
+  float* dl = lufs_inst;
+  int e = 0;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 0, x, (size_t)n * m * sizeof(float), reinterpret_cast<const void**>(&dx));
+    if (!e) e = stage_out(c, 5, weighted, (size_t)n * m, outs, &dw);
+    if (!e) e = stage_out(c, 2, lufs_inst, n, outs, &dl);
+    if (e) return e;
+  }
+  BiquadTab* tabs = nullptr;
+  e = get_kw_tab(c, m, &tabs);
+  if (e) return e;
+  KWeightParams kp{dx, m, 0, 1, n, tabs, tabs + 1, dl, dw, mode};
+  HIPC(c, launch_kweight(m, kp, c->stream));
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db, int64_t n_frames, double* meters,
+                       int mem) {
+  if (!c || !lufs_inst || !tp_db || !meters) return OMEGA_EINVAL;
+  if (n_frames <= 0) return n_frames == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  HIPC(c, hipSetDevice(c->device));
+  const int64_t ncf = n_frames * c->cfg.n_channels;
+  std::vector<HostOut> outs;
+  const float* dl = lufs_inst;
+  const float* dt = tp_db;
+  double* dm = meters;
+  int e = 0;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 2, lufs_inst, ncf * sizeof(float), reinterpret_cast<const void**>(&dl));
+    if (!e) e = stage_in(c, 3, tp_db, ncf * sizeof(float), reinterpret_cast<const void**>(&dt));
+    if (!e) e = stage_out(c, 4, meters, ncf * 5, outs, &dm);
+    if (e) return e;
+  }
+  e = meters_enqueue(c, dl, dt, n_frames, dm);
+  if (e) return e;
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+int omega_bands_create(omega_ctx* c, int op, const int32_t* starts, const int32_t* ends, int32_t n_bands,
+                       int32_t n_out, const double* scale, const double* bin_scale, int32_t n_bins, omega_bands** out) {
+  if (!c || !starts || !ends || !out || n_bands < 0 || n_out < 0 || n_bins <= 0) return OMEGA_EINVAL;
+  if (op != OMEGA_BANDS_MAX && op != OMEGA_BANDS_MEAN) return fail(c, OMEGA_EINVAL, "unknown band op %d", op);
+  HIPC(c, hipSetDevice(c->device));
+  omega_bands* b = new (std::nothrow) omega_bands();
+  if (!b) return OMEGA_ENOMEM;
+  b->ctx = c;
+  b->op = op;
+  b->n_bands = n_bands;
+  b->n_out = n_out;
+  b->n_bins = n_bins;
+  // MAX (pipeline.py:207-220): bands min(num_bands, len(table)); each one that fits the spectrum.
+  // MEAN (freq_mapper.py:184-194): stops at the first band running past the spectrum.
+  int nv = std::min(n_bands, n_out);
+  if (op == OMEGA_BANDS_MEAN) {
+    for (int i = 0; i < nv; ++i)
+      if (ends[i] > n_bins) {
+        nv = i;
+        break;
+      }
+  }
+  b->n_valid = nv;
+  std::vector<int32_t> s(starts, starts + n_bands), en(ends, ends + n_bands);
+  if (s.empty()) {
+    s.push_back(0);
+    en.push_back(1);
+  }
+  int e = upload(c, &b->d_starts, s);
+  if (!e) e = upload(c, &b->d_ends, en);
+  b->d_scale = nullptr;
+  b->d_bin_scale = nullptr;
+  if (!e && scale) {
+    std::vector<float> sc(std::max(n_out, 1), 1.0f);
+    for (int i = 0; i < std::min(n_bands, n_out); ++i) sc[i] = (float)scale[i];
+    e = upload(c, &b->d_scale, sc);
+  }
+  if (!e && bin_scale) {
+    std::vector<float> bs(bin_scale, bin_scale + n_bins);
+    e = upload(c, &b->d_bin_scale, bs);
+  }
+  if (e) {
+    delete b;
+    return e;
+  }
+  *out = b;
+  return 0;
+}
+
+void omega_bands_destroy(omega_bands* b) { delete b; }  // device tables are owned by the context
+
+int omega_bands_apply(omega_ctx* c, omega_bands* b, const float* spec, int64_t n, int64_t spec_stride, float* out,
+                      int mem) {
+  if (!c || !b || !spec || !out) return OMEGA_EINVAL;
+  if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  HIPC(c, hipSetDevice(c->device));
+  std::vector<HostOut> outs;
+  const float* ds = spec;
+  float* dout = out;
+  int e = 0;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 0, spec, ((n - 1) * spec_stride + b->n_bins) * sizeof(float), reinterpret_cast<const void**>(&ds));
+    if (!e) e = stage_out(c, 1, out, (size_t)n * b->n_out, outs, &dout);
+    if (e) return e;
+  }
+  BandParams p{ds, n, spec_stride, b->n_bins, b->n_out, b->d_starts, b->d_ends, b->d_scale, b->d_bin_scale, b->op,
+               b->n_valid, dout};
+  HIPC(c, launch_bands(p, c->stream));
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+int omega_chroma(omega_ctx* c, const float* spec, int64_t n, int32_t n_bins, double df, double* out_raw, int mem) {
+  if (!c || !spec || !out_raw || n_bins < 3 || !(df > 0)) return OMEGA_EINVAL;
+  if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  HIPC(c, hipSetDevice(c->device));
+  auto it = c->chroma_mats.find(n_bins);
+  if (it == c->chroma_mats.end() || c->chroma_df != df) {
+    // chromagram.py:122-146 with transposition offset 0: bins 20 < f < 8000
+    int lo = n_bins, hi = 0;
+    for (int k = 0; k < n_bins; ++k) {
+      const double f = k * df;
+      if (f > 20 && f < 8000) {
+        lo = std::min(lo, k);
+        hi = std::max(hi, k + 1);
+      }
+    }
+    if (hi <= lo) lo = hi = 0;
+    const int nb = std::max(hi - lo, 1);
+    std::vector<double> m(12 * (size_t)nb, 0.0);
+    for (int k = lo; k < hi; ++k) {
+      const double f = k * df;
+      const double midi = 69 + 12 * std::log2(f / 440.0);
+      double cb = std::fmod(midi, 12.0);
+      if (cb < 0) cb += 12.0;
+      const int base = (int)cb;
+      const double sw = f < 100 ? 0.5 : (f < 1000 ? 1.0 : (f < 4000 ? 0.8 : 0.6));
+      for (int o = -2; o <= 2; ++o) {
+        const int tb = ((base + o) % 12 + 12) % 12;
+        const double d = std::fabs(cb - (base + o));
+        const double w = std::exp(-0.5 * (d / 0.5) * (d / 0.5));
+        m[(size_t)tb * nb + (k - lo)] += w * sw;
+      }
+    }
+    double* d = nullptr;
+    HIPC(c, hipMalloc(&d, m.size() * sizeof(double)));
+    HIPC(c, hipMemcpy(d, m.data(), m.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (it != c->chroma_mats.end()) (void)hipFree(it->second.first);
+    c->chroma_mats[n_bins] = {d, {lo, hi}};
+    c->chroma_df = df;
+    it = c->chroma_mats.find(n_bins);
+  }
+  std::vector<HostOut> outs;
+  const float* ds = spec;
+  double* dout = out_raw;
+  int e = 0;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 0, spec, (size_t)n * n_bins * sizeof(float), reinterpret_cast<const void**>(&ds));
+    if (!e) e = stage_out(c, 1, out_raw, (size_t)n * 12, outs, &dout);
+    if (e) return e;
+  }
+  HIPC(c, launch_chroma(ds, n, n_bins, it->second.second.first, it->second.second.second, it->second.first, dout,
+                        c->stream));
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+int omega_rfft(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t window, float* mag, float* cplx, int mem) {
+  if (!c || !x || (!mag && !cplx)) return OMEGA_EINVAL;
+  if (!is_pow2_in(m, 512, 16384)) return fail(c, OMEGA_EUNSUP, "rfft: length %d unsupported", m);
+  if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  HIPC(c, hipSetDevice(c->device));
+  float* win = nullptr;
+  int e = get_window(c, m, window, &win);
+  if (e) return e;
+  std::vector<HostOut> outs;
+  const float* dx = x;
+  float* dm = mag;
+  float* dc = cplx;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 0, x, (size_t)n * m * sizeof(float), reinterpret_cast<const void**>(&dx));
+    if (!e) e = stage_out(c, 1, mag, (size_t)n * (m / 2 + 1), outs, &dm);
+    if (!e) e = stage_out(c, 2, cplx, (size_t)n * (m / 2 + 1) * 2, outs, &dc);
+    if (e) return e;
+  }
+  RfftParams p{};
+  p.x = dx;
+  p.n = n;
+  p.win = win;
+  p.mag = dm;
+  p.cplx = dc;
+  for (int l = 0; l < kMaxLog2; ++l) p.tw[l] = c->d_tw[l];
+  HIPC(c, launch_rfft(m, p, c->stream));
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+}  // extern "C"

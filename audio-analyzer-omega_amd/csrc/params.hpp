@@ -1,0 +1,140 @@
+// Kernel parameter blocks shared by the host launcher (capi.cpp) and the device code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace omega {
+
+constexpr int kMaxRes = 4;
+constexpr int kMaxLog2 = 15;  // twiddle tables for sizes 2^1 .. 2^14 (+1 spare)
+
+// One resolution of the multi-resolution FFT (FFTConfig, multi_resolution_fft.py:26-44).
+struct ResParam {
+  int n;                 // real FFT size N_r
+  int offset;            // W - N_r: the resolution reads the last N_r samples of the frame
+  const float* win;      // [N_r] window (np.blackman(N).astype(f32))
+  const float* wgt;      // [N_r/2+1] psychoacoustic weights (ones if apply_weighting is off)
+  float* mag_out;        // [n_cf, N_r/2+1] or nullptr
+  int ent_begin, ent_end;  // this resolution's combine entries
+  float cw;              // combine weight (config.weight)
+};
+
+struct SpectralParams {
+  const float* x;
+  int64_t frame_stride, chan_stride;
+  int C;
+  int64_t n_cf;
+  int n_res;
+  ResParam res[kMaxRes];
+  // combine plan (multi_resolution_fft.py:353-395): entry e adds cw * interp to target ent_t[e]
+  const int* ent_t;
+  const int* ent_j;
+  const float* ent_frac;
+  const float* wsum;  // [T] weight sum per target (0 -> output 0)
+  int T;
+  float* comb_out;    // [n_cf, T] or nullptr
+  // true peak (professional_meters.py:283-299)
+  float* tp_out;      // [n_cf] or nullptr
+  const float2* rot;  // [W/2 + 1] exp(+2 pi i k / (4W))
+  const float2* tw[kMaxLog2];  // tw[l][m] = exp(-2 pi i m / 2^l)
+};
+
+// One zero-phase biquad (filtfilt with scipy's defaults) in state-space form:
+// s' = A s + B u, y = s0 + b0 u, A = [[-a1, 1], [-a2, 0]], B = [b1 - a1 b0, b2 - a2 b0].
+struct BiquadTab {
+  float b0, a1, a2, B0, B1;
+  float zi0, zi1;      // scipy.signal.lfilter_zi
+  float h0[64], h1[64];  // first row of A^n, n < L (zero-input response of a chunk)
+  float pw[64][4];     // P^(l+1), P = A^L, row-major 2x2
+};
+
+struct KWeightParams {
+  const float* x;
+  int64_t frame_stride, chan_stride;
+  int C;
+  int64_t n_cf;
+  const BiquadTab* hp;     // 38 Hz Butterworth high-pass (professional_meters.py:52-54)
+  const BiquadTab* shelf;  // 1500 Hz Butterworth high-pass "shelf" (:56-64)
+  float* lufs_out;         // [n_cf] or nullptr
+  float* weighted_out;     // [n_cf, M] or nullptr
+  int mode;                // 0: K-weighting, 3: Z (no filter, no gate: professional_meters.py:228-229)
+};
+
+struct MeterParams {
+  const float* lufs;   // [n_frames * C] batch instantaneous LUFS
+  const float* tp;     // [n_frames * C]
+  int64_t n_frames;
+  int C;
+  const float* hist_l;  // [C, HL] previous LUFS_inst values, oldest first
+  const float* hist_t;  // [C, HT] previous true-peak values
+  const int* n_hist_l;  // [C]
+  const int* n_hist_t;  // [C]
+  int HL, HT;           // capacities: integrated_len - 1, peak_len - 1
+  int mom_len, short_len, int_len, peak_len;
+  float gate;
+  double* out;          // [n_frames * C, 5]
+};
+
+struct MeterStateParams {
+  const float* lufs;
+  const float* tp;
+  int64_t n_frames;
+  int C;
+  const float* hist_l_in;
+  const float* hist_t_in;
+  const int* n_l_in;
+  const int* n_t_in;
+  float* hist_l_out;
+  float* hist_t_out;
+  int* n_l_out;
+  int* n_t_out;
+  int HL, HT;
+};
+
+struct BandParams {
+  const float* spec;
+  int64_t n, spec_stride;
+  int n_bins;
+  int n_out;
+  const int* starts;
+  const int* ends;
+  const float* scale;      // [n_out] per-band multiplier (MAX) or nullptr
+  const float* bin_scale;  // [n_bins] per-bin multiplier (MEAN) or nullptr
+  int op;                  // 0 max, 1 mean
+  int n_valid;             // bands computed; the rest are 0
+  float* out;              // [n, n_out]
+};
+
+struct ChromaParams {
+  const float* spec;
+  int64_t n;
+  int n_bins;
+  double df;
+  const float* mat;     // [12, n_bins] projection (chromagram.py:122-146), zero outside 20..8000 Hz
+  double* out;          // [n, 12] normalised smoothed chroma (before the temporal blend)
+};
+
+// combine_results_optimized over externally supplied (already weighted) magnitudes; a missing
+// resolution (mag[r] == nullptr) is skipped like a key absent from the results dict.
+struct CombineParams {
+  const float* mag[kMaxRes];
+  int nbins[kMaxRes];
+  float cw[kMaxRes];
+  int64_t n_cf;
+  int T;
+  const int* own_off;   // [T+1]
+  const int* own_rj;    // (r << 24) | j
+  const float* own_frac;
+  float* out;           // [n_cf, T]
+};
+
+struct RfftParams {
+  const float* x;
+  int64_t n;
+  const float* win;
+  float* mag;    // [n, m/2+1] or nullptr
+  float* cplx;   // [n, m/2+1, 2] or nullptr
+  const float2* tw[kMaxLog2];
+};
+
+}  // namespace omega

@@ -1,0 +1,321 @@
+// Spectral kernels: one 256-thread workgroup (4 wave64s) per channel-frame.
+//
+//   A3/A4  multi_resolution_fft.py:264-279  window * last N_r samples -> rfft -> |.| * weight
+//   A5     multi_resolution_fft.py:353-395  interpolated combine onto linspace(0, max_freq, T)
+//   A8     professional_meters.py:283-299  4x FFT-resample true peak (polyphase form)
+//   A13    batched_fft_processor.py:148-285 windowed rfft -> magnitude / complex
+//
+// Every real FFT of N points is a complex FFT of K = N/2 points on z[n] = x[2n] + i x[2n+1]
+// followed by the standard untangle X[k] = E_k + W_N^k O_k. The true peak never forms the 4M-point
+// inverse FFT scipy.signal.resample uses: with X = rfft_M(x), the oversampled signal is
+//   y[4n+p] = irfft_M( X_k e^{2 pi i k p / 4M} ), Nyquist bin -> X_{M/2} cos(pi p / 4),
+// so it costs one rfft(M) plus three irfft(M) (p = 1..3; p = 0 is x itself), each an M/2-point
+// complex FFT that fits a 64 KiB LDS buffer (identity checked in tests/test_algorithm_identities.py).
+//
+// One kernel per resolution size keeps each kernel's register allocation to one FFT instance
+// (a single kernel looping over four sizes spilled); the frame stays L2/MALL-resident between the
+// resolution kernels of one batch.
+#include "fft.hpp"
+#include "params.hpp"
+
+namespace omega {
+
+__device__ __forceinline__ float cabs(float2 z) { return sqrtf(fmaf(z.x, z.x, z.y * z.y)); }
+
+// untangle of one pair (k, K-k), 0 < k < K/2: returns X[k] and X[K-k]
+__device__ __forceinline__ void untangle(float2 a, float2 b, float2 w, float2& xk, float2& xkk) {
+  // E = (a + conj b)/2, O = -i (a - conj b)/2, X[k] = E + w O, X[K-k] = conj(E - w O)
+  const float2 E = make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+  const float2 O = make_float2(0.5f * (a.y + b.y), -0.5f * (a.x - b.x));
+  const float2 wo = cmul(w, O);
+  xk = cadd(E, wo);
+  xkk = cconj(csub(E, wo));
+}
+
+// |X[k]| of the rfft of N = 2K real points lands at float index magidx<K>(k) of buf.
+template <int K, int NTH>
+__device__ __forceinline__ int magidx(int k) {
+  return k == K ? 2 * BlockFFT<K, NTH>::out(0) : 2 * BlockFFT<K, NTH>::out(k) + 1;
+}
+
+// Magnitudes from the packed complex FFT in buf (BlockFFT<K> output order). Pair (k, K-k) is owned
+// by one thread, which overwrites only the imaginary slots of the two entries it read: no barrier
+// between reads and writes, nothing held in registers.
+template <int K, int NTH>
+__device__ __forceinline__ void rfft_magnitudes(float2* buf, const float2* __restrict__ twN, int tid) {
+  using FFT = BlockFFT<K, NTH>;
+  float* mag = reinterpret_cast<float*>(buf);
+  for (int k = tid; k < K / 2; k += NTH) {
+    if (k == 0) {
+      const float2 z = buf[FFT::out(0)];
+      const float2 zm = buf[FFT::out(K / 2)];
+      mag[magidx<K, NTH>(0)] = fabsf(z.x + z.y);
+      mag[magidx<K, NTH>(K)] = fabsf(z.x - z.y);
+      mag[magidx<K, NTH>(K / 2)] = cabs(zm);  // X[K/2] = conj(Z[K/2])
+    } else {
+      float2 xk, xkk;
+      untangle(buf[FFT::out(k)], buf[FFT::out(K - k)], twN[k], xk, xkk);
+      mag[magidx<K, NTH>(k)] = cabs(xk);
+      mag[magidx<K, NTH>(K - k)] = cabs(xkk);
+    }
+  }
+  __syncthreads();
+}
+
+// Multi-resolution kernel for one resolution of K = N_r/2 complex points (A3-A5). Launched once per
+// resolution, in resolution order. Combine entries carry a mode (the per-target restatement of
+// multi_resolution_fft.py:387-395):
+//   0: out = v*cw/wsum (sole owner)   1: out = v*cw (first of several owners)
+//   2: out += v*cw (middle owner)     3: out = (out + v*cw)/wsum (last owner)   4: out = 0 (no owner)
+template <int K, int NTH = threads_for<K>()>
+__global__ __launch_bounds__(NTH, 2 * NTH / 256) void mrfft_kernel(SpectralParams p, int r) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float2* buf = reinterpret_cast<float2*>(smem);
+  const int tid = threadIdx.x;
+  const int64_t cf = blockIdx.x;
+  const int64_t f = cf / p.C, c = cf % p.C;
+  const ResParam& rp = p.res[r];
+  const float* __restrict__ x = p.x + f * p.frame_stride + c * p.chan_stride + rp.offset;
+  const float2* x2 = reinterpret_cast<const float2*>(x);
+  const float2* w2 = reinterpret_cast<const float2*>(rp.win);
+  for (int n = tid; n < K; n += NTH) {
+    const float2 a = x2[n], w = w2[n];
+    buf[n] = make_float2(a.x * w.x, a.y * w.y);
+  }
+  __syncthreads();
+  BlockFFT<K, NTH>::run(buf, p.tw[ilog2(K)], tid);
+  rfft_magnitudes<K, NTH>(buf, p.tw[ilog2(2 * K)], tid);
+  const float* mag = reinterpret_cast<const float*>(buf);
+  const float* __restrict__ wgt = rp.wgt;
+  if (rp.mag_out) {
+    float* o = rp.mag_out + cf * (K + 1);
+    for (int k = tid; k <= K; k += NTH) o[k] = mag[magidx<K, NTH>(k)] * wgt[k];
+  }
+  if (p.comb_out) {
+    float* o = p.comb_out + cf * p.T;
+    for (int e = rp.ent_begin + tid; e < rp.ent_end; e += NTH) {
+      const int te = p.ent_t[e];
+      const int t = te & 0xFFFFFF, mode = te >> 24;
+      if (mode == 4) {
+        o[t] = 0.f;
+        continue;
+      }
+      const int j = p.ent_j[e];
+      const float fr = p.ent_frac[e];
+      const float m0 = mag[magidx<K, NTH>(j)] * wgt[j];
+      const float v = (fr != 0.f ? fmaf(fr, mag[magidx<K, NTH>(j + 1)] * wgt[j + 1] - m0, m0) : m0) * rp.cw;
+      if (mode == 0)
+        o[t] = v / p.wsum[t];
+      else if (mode == 1)
+        o[t] = v;
+      else if (mode == 2)
+        o[t] += v;
+      else
+        o[t] = (o[t] + v) / p.wsum[t];
+    }
+  }
+}
+
+// True peak of one frame of M = 2K samples (dBTP; float32 like scipy on float32 input).
+// (K = 8192 with 512 threads needs ~160 VGPRs: one 8-wave workgroup per CU, launch bound 2 waves/SIMD)
+template <int K, int NTH = threads_for<K>()>
+__global__ __launch_bounds__(NTH, K >= 8192 ? 2 : 2 * NTH / 256) void truepeak_kernel(SpectralParams p) {
+  constexpr int M = 2 * K;
+  using FFT = BlockFFT<K, NTH>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float2* buf = reinterpret_cast<float2*>(smem);
+  float* red = reinterpret_cast<float*>(smem + K * sizeof(float2));
+  const int tid = threadIdx.x;
+  const int64_t cf = blockIdx.x;
+  const int64_t f = cf / p.C, c = cf % p.C;
+  const float2* x2 = reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride);
+  float mx = 0.f;
+  for (int n = tid; n < K; n += NTH) {
+    const float2 a = x2[n];
+    buf[n] = a;
+    mx = fmaxf(mx, fmaxf(fabsf(a.x), fabsf(a.y)));
+  }
+  __syncthreads();
+  FFT::run(buf, p.tw[ilog2(K)], tid);
+  const float2* __restrict__ twM = p.tw[ilog2(M)];
+  constexpr int NP = K / 2;  // pairs (k, K-k), k < K/2; k = 0 carries X[0], X[K] and X[K/2]
+  constexpr int PB = (NP + NTH - 1) / NTH;
+  float2 Xlo[PB], Xhi[PB];
+  float2 Xmid = make_float2(0.f, 0.f);
+  static_for<0, PB>([&](auto b) {
+    const int k = tid + b * NTH;
+    if (NP % NTH == 0 || k < NP) {
+      // branch-free selects keep Xlo/Xhi in registers (a conditional write through a reference
+      // to an array element sent the arrays to scratch)
+      const int kk = k == 0 ? K / 2 : K - k;
+      const float2 a = buf[FFT::out(k)], bz = buf[FFT::out(kk)];
+      float2 lo, hi;
+      untangle(a, bz, twM[k], lo, hi);
+      if (k == 0) Xmid = cconj(bz);
+      Xlo[b] = k == 0 ? make_float2(a.x + a.y, 0.f) : lo;
+      Xhi[b] = k == 0 ? make_float2(a.x - a.y, 0.f) : hi;
+    }
+  });
+  const float2* rot = p.rot;  // e^{2 pi i k / 4M}, k <= K
+  constexpr float kS2 = 7.071067812e-01f;
+  float fmx = 0.f;
+#pragma unroll 1
+  for (int P = 1; P <= 3; ++P) {
+    // opaque per-iteration table pointers: stop LICM from hoisting (and keeping live across the
+    // loop) every twiddle and rotation load of the three inverse transforms
+    // (tid is laundered too: otherwise every LDS address of the inlined FFT, a function of tid
+    // alone, is hoisted out of the loop and pinned in VGPRs)
+    const float2* twK = p.tw[ilog2(K)];
+    int tl = tid;
+    asm volatile("" : "+s"(twK), "+s"(rot), "+v"(tl));
+    __syncthreads();  // the previous readers of buf are done
+    const float nyq = P == 2 ? 0.f : (P == 1 ? kS2 : -kS2);  // cos(pi P / 4)
+    static_for<0, PB>([&](auto b) {
+      const int k = tl + b * NTH;
+      if (NP % NTH == 0 || k < NP) {
+        const float2 r1 = rot[k];
+        const float2 r2 = cmul(r1, r1);
+        const float2 rp = P == 1 ? r1 : (P == 2 ? r2 : cmul(r2, r1));
+        const float2 e = cmul(r2, r2);  // e^{2 pi i k / M}
+        const float2 q1 = cmul(make_float2(kS2, kS2), cconj(r1));  // e^{2 pi i (K-k) / 4M}
+        const float2 q2 = cmul(q1, q1);
+        const float2 qp = P == 1 ? q1 : (P == 2 ? q2 : cmul(q2, q1));
+        const float2 yk = cmul(Xlo[b], rp);
+        const float2 ykk = (k == 0) ? make_float2(Xhi[b].x * nyq, 0.f) : cmul(Xhi[b], qp);
+        // Z'[k] = E + iO, Z'[K-k] = conj(E) + i conj(O); E = (Y_k + conj Y_{K-k})/2,
+        // O = (Y_k - conj Y_{K-k})/2 e. Stored conjugated: a forward FFT then gives conj(ifft).
+        const float2 E = make_float2(0.5f * (yk.x + ykk.x), 0.5f * (yk.y - ykk.y));
+        const float2 O = cmul(make_float2(0.5f * (yk.x - ykk.x), 0.5f * (yk.y + ykk.y)), e);
+        buf[k] = make_float2(E.x - O.y, -(E.y + O.x));
+        if (k != 0) {
+          buf[K - k] = make_float2(E.x + O.y, E.y - O.x);
+        } else {
+          // k = K/2: Z'[K/2] = conj(Y[K/2]), Y[K/2] = X[K/2] rot^P(K/2); stored conjugated = Y
+          const float2 rh = rot[K / 2];
+          const float2 rh2 = cmul(rh, rh);
+          buf[K / 2] = cmul(Xmid, P == 1 ? rh : (P == 2 ? rh2 : cmul(rh2, rh)));
+        }
+      }
+    });
+    __syncthreads();
+    FFT::run(buf, twK, tl);
+    for (int n = tl; n < K; n += NTH) {
+      const float2 z = buf[n];
+      fmx = fmaxf(fmx, fmaxf(fabsf(z.x), fabsf(z.y)));
+    }
+  }
+  const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
+  if (tid == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
+}
+
+// Standalone windowed rfft (A13): magnitude and/or complex spectrum.
+template <int K, int NTH = threads_for<K>()>
+__global__ __launch_bounds__(NTH, 2 * NTH / 256) void rfft_kernel(RfftParams p) {
+  using FFT = BlockFFT<K, NTH>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float2* buf = reinterpret_cast<float2*>(smem);
+  const int tid = threadIdx.x;
+  const int64_t i = blockIdx.x;
+  const float2* x2 = reinterpret_cast<const float2*>(p.x + i * (2 * K));
+  const float2* w2 = reinterpret_cast<const float2*>(p.win);
+  for (int n = tid; n < K; n += NTH) {
+    const float2 a = x2[n], w = w2[n];
+    buf[n] = make_float2(a.x * w.x, a.y * w.y);
+  }
+  __syncthreads();
+  FFT::run(buf, p.tw[ilog2(K)], tid);
+  const float2* __restrict__ twN = p.tw[ilog2(2 * K)];
+  float2* cp = p.cplx ? reinterpret_cast<float2*>(p.cplx) + i * (K + 1) : nullptr;
+  float* mp = p.mag ? p.mag + i * (K + 1) : nullptr;
+  for (int k = tid; k < K / 2; k += NTH) {
+    float2 xk, xkk;
+    if (k == 0) {
+      const float2 z = buf[FFT::out(0)];
+      xk = make_float2(z.x + z.y, 0.f);
+      xkk = make_float2(z.x - z.y, 0.f);
+      const float2 xm = cconj(buf[FFT::out(K / 2)]);
+      if (cp) cp[K / 2] = xm;
+      if (mp) mp[K / 2] = cabs(xm);
+    } else {
+      untangle(buf[FFT::out(k)], buf[FFT::out(K - k)], twN[k], xk, xkk);
+    }
+    if (cp) {
+      cp[k] = xk;
+      cp[K - k] = xkk;
+    }
+    if (mp) {
+      mp[k] = cabs(xk);
+      mp[K - k] = cabs(xkk);
+    }
+  }
+}
+
+// combine_results_optimized over given magnitudes: thread per target bin, owners in resolution
+// order, float32 accumulators as the reference's pool arrays (multi_resolution_fft.py:355-395).
+__global__ __launch_bounds__(256) void combine_kernel(CombineParams p) {
+  const int64_t cf = blockIdx.y;
+  for (int t = blockIdx.x * 256 + threadIdx.x; t < p.T; t += gridDim.x * 256) {
+    float acc = 0.f, ws = 0.f;
+    for (int q = p.own_off[t]; q < p.own_off[t + 1]; ++q) {
+      const int rj = p.own_rj[q];
+      const int r = rj >> 24, j = rj & 0xFFFFFF;
+      const float* m = p.mag[r];
+      if (!m) continue;
+      m += cf * p.nbins[r];
+      const float fr = p.own_frac[q];
+      const float v = fr != 0.f ? fmaf(fr, m[j + 1] - m[j], m[j]) : m[j];
+      acc = fmaf(v, p.cw[r], acc);
+      ws += p.cw[r];
+    }
+    p.out[cf * p.T + t] = ws > 0.f ? acc / ws : 0.f;
+  }
+}
+
+// ---- host launchers ----
+#define OMEGA_SWITCH_K(n, CALL) \
+  switch (n) {                  \
+    case 512: CALL(256); break;   \
+    case 1024: CALL(512); break;  \
+    case 2048: CALL(1024); break; \
+    case 4096: CALL(2048); break; \
+    case 8192: CALL(4096); break; \
+    case 16384: CALL(8192); break; \
+    default: return hipErrorInvalidValue; \
+  }
+
+// Resolution kernels (in resolution order), then the true-peak kernel for frames of W samples.
+hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)p.n_cf);
+  for (int r = 0; r < p.n_res; ++r) {
+    if (!p.comb_out && !p.res[r].mag_out) continue;
+#define OMEGA_RES(K) \
+  hipLaunchKernelGGL(mrfft_kernel<K>, grid, dim3(threads_for<K>()), K * sizeof(float2), s, p, r)
+    OMEGA_SWITCH_K(p.res[r].n, OMEGA_RES)
+#undef OMEGA_RES
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (p.tp_out) {
+#define OMEGA_TP(K) \
+  hipLaunchKernelGGL(truepeak_kernel<K>, grid, dim3(threads_for<K>()), K * sizeof(float2) + 16 * sizeof(float), \
+                     s, p)
+    OMEGA_SWITCH_K(W, OMEGA_TP)
+#undef OMEGA_TP
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_combine(const CombineParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(combine_kernel, dim3((unsigned)((p.T + 255) / 256), (unsigned)p.n_cf), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)p.n);
+#define OMEGA_RF(K) hipLaunchKernelGGL(rfft_kernel<K>, grid, dim3(threads_for<K>()), K * sizeof(float2), s, p)
+  OMEGA_SWITCH_K(m, OMEGA_RF)
+#undef OMEGA_RF
+  return hipGetLastError();
+}
+
+}  // namespace omega

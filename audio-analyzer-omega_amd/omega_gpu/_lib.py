@@ -1,0 +1,99 @@
+"""ctypes binding of libomega.so (include/omega.h). No torch types cross this boundary: plain
+pointers and sizes. The library is loaded from the package's in-tree ``lib/`` and the import fails
+loudly when it is missing -- there is no CPU fallback."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libomega.so")
+
+MAX_RES = 4
+N_METERS = 5
+MEM_HOST, MEM_DEVICE = 0, 1
+WIN = {"blackman": 0, "hann": 1, "hamming": 2, "rect": 3}
+BANDS_MAX, BANDS_MEAN = 0, 1
+WEIGHT = {"K": 0, "A": 1, "C": 2, "Z": 3}
+OK, EINVAL, EHIP, ENOMEM, EUNSUP = 0, -1, -2, -3, -4
+
+
+class Resolution(C.Structure):
+    _fields_ = [("freq_lo", C.c_double), ("freq_hi", C.c_double), ("fft_size", C.c_int32),
+                ("hop_size", C.c_int32), ("weight", C.c_double), ("window", C.c_int32)]
+
+
+class Config(C.Structure):
+    _fields_ = [("sample_rate", C.c_int32), ("max_freq", C.c_double), ("n_res", C.c_int32),
+                ("res", Resolution * MAX_RES), ("apply_weighting", C.c_int32), ("target_bins", C.c_int32),
+                ("frame_size", C.c_int32), ("n_channels", C.c_int32), ("gate_lufs", C.c_double),
+                ("momentary_len", C.c_int32), ("short_len", C.c_int32), ("integrated_len", C.c_int32),
+                ("peak_len", C.c_int32)]
+
+
+class Outputs(C.Structure):
+    _fields_ = [("combined", C.c_void_p), ("lufs_inst", C.c_void_p), ("true_peak_db", C.c_void_p),
+                ("meters", C.c_void_p), ("mag", C.c_void_p * MAX_RES), ("weighted", C.c_void_p)]
+
+
+class OmegaError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libomega error {code}: {msg}")
+        self.code = code
+
+
+class UnsupportedError(OmegaError):
+    """A valid reference call this build does not cover (e.g. a non power-of-two frame)."""
+
+
+EXPORTS = {
+    "omega_version": (C.c_char_p, []),
+    "omega_config_default": (None, [C.POINTER(Config)]),
+    "omega_create": (C.c_int, [C.POINTER(Config), C.c_int, C.POINTER(C.c_void_p)]),
+    "omega_destroy": (None, [C.c_void_p]),
+    "omega_last_error": (C.c_char_p, [C.c_void_p]),
+    "omega_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "omega_synchronize": (C.c_int, [C.c_void_p]),
+    "omega_process_frames": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64,
+                                       C.POINTER(Outputs), C.c_int]),
+    "omega_combine": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int64, C.c_void_p, C.c_int]),
+    "omega_true_peak": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int]),
+    "omega_k_weighting": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p,
+                                    C.c_int]),
+    "omega_weighting": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p,
+                                  C.c_void_p, C.c_int]),
+    "omega_meter_update": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
+    "omega_meter_reset": (C.c_int, [C.c_void_p]),
+    "omega_bands_create": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                     C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
+    "omega_bands_destroy": (None, [C.c_void_p]),
+    "omega_bands_apply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
+                                    C.c_int]),
+    "omega_chroma": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_double, C.c_void_p, C.c_int]),
+    "omega_rfft": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                             C.c_int]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libomega.so once (raises if the HIP library was not built: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libomega.so not found at {LIB_PATH}; run `make -C audio-analyzer-omega_amd` "
+                              "(or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(ctx, code: int) -> None:
+    if code != OK:
+        msg = lib().omega_last_error(ctx).decode() if ctx else ""
+        raise (UnsupportedError if code == EUNSUP else OmegaError)(code, msg)

@@ -1,0 +1,246 @@
+"""Engine: one libomega context (one HIP stream + per-channel meter state) and the batched
+entry points. Inputs may be numpy arrays (host memory: the call stages through device buffers and
+returns host arrays) or torch tensors on an MI355X (device memory: the call enqueues on torch's
+current stream and returns device tensors). torch is used only as a device-memory/stream carrier."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass(frozen=True)
+class Resolution:
+    """One FFT resolution (FFTConfig, multi_resolution_fft.py:26-44)."""
+
+    freq_range: Tuple[float, float]
+    fft_size: int
+    hop_size: int
+    weight: float
+    window: str = "blackman"
+
+
+DEFAULT_RESOLUTIONS = (  # multi_resolution_fft.py:149-154
+    Resolution((20, 200), 4096, 1024, 1.5),
+    Resolution((200, 1000), 2048, 512, 1.2),
+    Resolution((1000, 5000), 1024, 256, 1.0),
+    Resolution((5000, 20000), 1024, 256, 1.5),
+)
+NORTHSTAR_RESOLUTIONS = (  # BASELINE.json north-star sizes, same ranges/weights
+    Resolution((20, 200), 16384, 1024, 1.5),
+    Resolution((200, 1000), 8192, 512, 1.2),
+    Resolution((1000, 5000), 4096, 256, 1.0),
+    Resolution((5000, 20000), 1024, 256, 1.5),
+)
+METER_KEYS = ("momentary", "short_term", "integrated", "range", "true_peak")
+
+
+def _is_torch(a) -> bool:
+    return hasattr(a, "data_ptr") and hasattr(a, "is_cuda")
+
+
+def _ptr(a) -> Optional[int]:
+    if a is None:
+        return None
+    if _is_torch(a):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+class Engine:
+    def __init__(self, resolutions: Sequence[Resolution] = DEFAULT_RESOLUTIONS, sample_rate: int = 48000,
+                 max_freq: float = 20000, target_bins: int = 1024, frame_size: Optional[int] = None,
+                 n_channels: int = 1, apply_weighting: bool = True, device: int = 0):
+        self._ctx = C.c_void_p()
+        cfg = L.Config()
+        lib = L.lib()
+        lib.omega_config_default(C.byref(cfg))
+        resolutions = list(resolutions)
+        cfg.sample_rate = int(sample_rate)
+        cfg.max_freq = float(max_freq)
+        cfg.n_res = len(resolutions)
+        if not 1 <= cfg.n_res <= L.MAX_RES:
+            raise ValueError(f"1..{L.MAX_RES} resolutions supported")
+        for i, r in enumerate(resolutions):
+            cfg.res[i] = L.Resolution(float(r.freq_range[0]), float(r.freq_range[1]), int(r.fft_size),
+                                      int(r.hop_size), float(r.weight), L.WIN.get(r.window, 0))
+        cfg.apply_weighting = 1 if apply_weighting else 0
+        cfg.target_bins = int(target_bins)
+        cfg.frame_size = int(frame_size or max(r.fft_size for r in resolutions))
+        cfg.n_channels = int(n_channels)
+        self.cfg = cfg
+        self.resolutions = tuple(resolutions)
+        self.W, self.C, self.T = cfg.frame_size, cfg.n_channels, cfg.target_bins
+        self.device = device
+        code = lib.omega_create(C.byref(cfg), int(device), C.byref(self._ctx))
+        if code != L.OK:
+            msg = lib.omega_last_error(self._ctx).decode()
+            lib.omega_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+            if code == L.EINVAL:
+                raise ValueError(msg)
+            raise (L.UnsupportedError if code == L.EUNSUP else L.OmegaError)(code, msg)
+
+    # -- lifecycle --
+    def close(self):
+        if self._ctx:
+            L.lib().omega_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, code):
+        L.check(self._ctx, code)
+
+    def synchronize(self):
+        self._check(L.lib().omega_synchronize(self._ctx))
+
+    def _bind_stream(self, tensor):
+        import torch
+        self._check(L.lib().omega_set_stream(self._ctx, C.c_void_p(torch.cuda.current_stream(tensor.device).cuda_stream)))
+
+    def reset_meters(self):
+        self._check(L.lib().omega_meter_reset(self._ctx))
+
+    # -- helpers --
+    def _alloc(self, like, shape, dtype):
+        if _is_torch(like):
+            import torch
+            tdt = {np.float32: torch.float32, np.float64: torch.float64}[dtype]
+            return torch.empty(shape, dtype=tdt, device=like.device)
+        return np.empty(shape, dtype=dtype)
+
+    # -- the fused per-channel-frame path --
+    def process_frames(self, x, n_frames: int, frame_stride: int, channel_stride: int, *, combined=True,
+                       lufs=True, true_peak=True, meters=False, mags=False, weighted=False,
+                       out: Optional[Dict] = None) -> Dict:
+        """Run the hot path over n_frames x n_channels channel-frames of x (flat float32, host numpy
+        or device torch). Returns a dict of the requested outputs (numpy or torch, like x)."""
+        dev = _is_torch(x)
+        if not dev:
+            x = np.ascontiguousarray(x, dtype=np.float32)
+        ncf = n_frames * self.C
+        o = dict(out or {})
+        if combined and "combined" not in o:
+            o["combined"] = self._alloc(x, (ncf, self.T), np.float32)
+        if lufs and "lufs_inst" not in o:
+            o["lufs_inst"] = self._alloc(x, (ncf,), np.float32)
+        if true_peak and "true_peak_db" not in o:
+            o["true_peak_db"] = self._alloc(x, (ncf,), np.float32)
+        if meters and "meters" not in o:
+            o["meters"] = self._alloc(x, (ncf, L.N_METERS), np.float64)
+        if weighted and "weighted" not in o:
+            o["weighted"] = self._alloc(x, (ncf, self.W), np.float32)
+        if mags:
+            sel = range(len(self.resolutions)) if mags is True else mags
+            for r in sel:
+                o.setdefault(f"mag{r}", self._alloc(x, (ncf, self.resolutions[r].fft_size // 2 + 1), np.float32))
+        outs = L.Outputs()
+        outs.combined = _ptr(o.get("combined"))
+        outs.lufs_inst = _ptr(o.get("lufs_inst"))
+        outs.true_peak_db = _ptr(o.get("true_peak_db"))
+        outs.meters = _ptr(o.get("meters"))
+        outs.weighted = _ptr(o.get("weighted"))
+        for r in range(len(self.resolutions)):
+            outs.mag[r] = _ptr(o.get(f"mag{r}"))
+        if dev:
+            self._bind_stream(x)
+        self._check(L.lib().omega_process_frames(self._ctx, _ptr(x), int(n_frames), int(frame_stride),
+                                                 int(channel_stride), C.byref(outs),
+                                                 L.MEM_DEVICE if dev else L.MEM_HOST))
+        return o
+
+    def combine(self, mags: Dict[int, np.ndarray], n_cf: int = 1) -> np.ndarray:
+        """combine_results_optimized on the device over the given weighted magnitudes."""
+        arrs = {i: np.ascontiguousarray(m, dtype=np.float32) for i, m in mags.items()}
+        ptrs = (C.c_void_p * L.MAX_RES)()
+        for i in range(L.MAX_RES):
+            ptrs[i] = arrs[i].ctypes.data if i in arrs else None
+        out = np.empty((n_cf, self.T), np.float32)
+        self._check(L.lib().omega_combine(self._ctx, ptrs, int(n_cf), out.ctypes.data, L.MEM_HOST))
+        return out
+
+    def true_peak(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float32)
+        out = np.empty(x.shape[0], np.float32)
+        self._check(L.lib().omega_true_peak(self._ctx, x.ctypes.data, x.shape[0], x.shape[1], out.ctypes.data,
+                                            L.MEM_HOST))
+        return out
+
+    def weighting(self, x: np.ndarray, mode: str = "K", weighted: bool = True):
+        """apply_weighting (+ instantaneous LUFS) for n frames [n, m]."""
+        x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float32)
+        w = np.empty_like(x) if weighted else None
+        li = np.empty(x.shape[0], np.float32)
+        self._check(L.lib().omega_weighting(self._ctx, x.ctypes.data, x.shape[0], x.shape[1], L.WEIGHT[mode],
+                                            w.ctypes.data if w is not None else None, li.ctypes.data, L.MEM_HOST))
+        return w, li
+
+    def k_weighting(self, x: np.ndarray, weighted: bool = True):
+        return self.weighting(x, "K", weighted)
+
+    def meter_update(self, lufs_inst, tp_db, n_frames: int) -> np.ndarray:
+        li = np.ascontiguousarray(lufs_inst, dtype=np.float32)
+        tp = np.ascontiguousarray(tp_db, dtype=np.float32)
+        out = np.empty((n_frames * self.C, L.N_METERS), np.float64)
+        self._check(L.lib().omega_meter_update(self._ctx, li.ctypes.data, tp.ctypes.data, int(n_frames),
+                                               out.ctypes.data, L.MEM_HOST))
+        return out
+
+    def rfft(self, x: np.ndarray, window: str = "hann", magnitude=True, complex_out=True):
+        x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float32)
+        n, m = x.shape
+        mag = np.empty((n, m // 2 + 1), np.float32) if magnitude else None
+        cp = np.empty((n, m // 2 + 1), np.complex64) if complex_out else None
+        self._check(L.lib().omega_rfft(self._ctx, x.ctypes.data, n, m, L.WIN.get(window, 3),
+                                       mag.ctypes.data if mag is not None else None,
+                                       cp.ctypes.data if cp is not None else None, L.MEM_HOST))
+        return mag, cp
+
+    def chroma_raw(self, spec: np.ndarray, df: float) -> np.ndarray:
+        s = np.ascontiguousarray(np.atleast_2d(spec), dtype=np.float32)
+        out = np.empty((s.shape[0], 12), np.float64)
+        self._check(L.lib().omega_chroma(self._ctx, s.ctypes.data, s.shape[0], s.shape[1], float(df),
+                                         out.ctypes.data, L.MEM_HOST))
+        return out
+
+
+class BandTable:
+    """A device band table bound to an engine (omega_bands_*)."""
+
+    def __init__(self, engine: Engine, op: int, starts, ends, n_out: int, n_bins: int, scale=None, bin_scale=None):
+        self.engine = engine
+        s = np.ascontiguousarray(starts, dtype=np.int32)
+        e = np.ascontiguousarray(ends, dtype=np.int32)
+        sc = None if scale is None else np.ascontiguousarray(scale, dtype=np.float64)
+        bs = None if bin_scale is None else np.ascontiguousarray(bin_scale, dtype=np.float64)
+        self.n_out, self.n_bins = int(n_out), int(n_bins)
+        self._h = C.c_void_p()
+        engine._check(L.lib().omega_bands_create(engine._ctx, op, s.ctypes.data, e.ctypes.data, len(s), self.n_out,
+                                                 sc.ctypes.data if sc is not None else None,
+                                                 bs.ctypes.data if bs is not None else None, self.n_bins,
+                                                 C.byref(self._h)))
+
+    def apply(self, spec: np.ndarray) -> np.ndarray:
+        s = np.ascontiguousarray(np.atleast_2d(spec), dtype=np.float32)
+        if s.shape[1] != self.n_bins:
+            raise ValueError(f"band table built for {self.n_bins} bins, got {s.shape[1]}")
+        out = np.empty((s.shape[0], self.n_out), np.float32)
+        self.engine._check(L.lib().omega_bands_apply(self.engine._ctx, self._h, s.ctypes.data, s.shape[0],
+                                                     s.shape[1], out.ctypes.data, L.MEM_HOST))
+        return out
+
+    def __del__(self):
+        try:
+            if self._h:
+                L.lib().omega_bands_destroy(self._h)
+        except Exception:
+            pass

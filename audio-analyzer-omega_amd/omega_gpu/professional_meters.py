@@ -1,0 +1,108 @@
+"""Drop-in ProfessionalMetering over libomega.so (omega4/panels/professional_meters.py:13-299).
+
+``calculate_lufs`` returns the same (mutated, shared) ``current_lufs`` dict with the same keys; the
+K-weighting, the instantaneous LUFS, the 4x true peak and the momentary / short-term / integrated /
+range / peak-hold deques all run on the MI355X (the deques live in the context as device-side
+per-stream history). Filter coefficients are derived in the library (closed forms of
+scipy.signal.butter / lfilter_zi) and exposed here for inspection.
+
+Frames must be a power of two between 512 and 16384 samples: other lengths (the reference accepts
+any length > 9) are logged and leave the meters unchanged -- see DESIGN.md 'Scope'.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict
+
+import numpy as np
+
+from .engine import Engine, Resolution
+from ._lib import UnsupportedError
+
+logger = logging.getLogger(__name__)
+
+_SUPPORTED = {512, 1024, 2048, 4096, 8192, 16384}
+
+
+def _butter2_highpass(fc: float, fs: float):
+    k = np.tan(np.pi * fc / fs)
+    n = 1 + np.sqrt(2) * k + k * k
+    return np.array([1.0, -2.0, 1.0]) / n, np.array([1.0, 2 * (k * k - 1) / n, (1 - np.sqrt(2) * k + k * k) / n])
+
+
+class ProfessionalMetering:
+    """Professional audio metering standards (LUFS, K-weighting, True Peak)."""
+
+    def __init__(self, sample_rate: int = 48000, device: int = 0):
+        self.sample_rate = sample_rate
+        self.gate_threshold = -70.0
+        self.weighting_mode = "K"
+        hp_b, hp_a = _butter2_highpass(38.0, sample_rate)
+        sh_b, sh_a = _butter2_highpass(1500.0, sample_rate)
+        self.k_weighting_filter = {"hp_b": hp_b, "hp_a": hp_a, "shelf_b": sh_b, "shelf_a": sh_a,
+                                   "shelf_gain": 10 ** (4.0 / 20)}
+        self.current_lufs = {"momentary": -100.0, "short_term": -100.0, "integrated": -100.0, "range": 0.0,
+                             "true_peak": -100.0}
+        self.current_true_peak = -100.0
+        # one context: its meter state is the four deques of :20-25 for one stream
+        self._eng = Engine([Resolution((20, 20000), 512, 256, 1.0)], sample_rate, min(20000, sample_rate / 2),
+                           target_bins=2, frame_size=512, n_channels=1, device=device)
+
+    def _frame(self, audio_data):
+        x = np.asarray(audio_data, dtype=np.float32).ravel()
+        if len(x) not in _SUPPORTED:
+            raise UnsupportedError(-4, f"frame length {len(x)} not supported (power of two 512..16384)")
+        return x
+
+    def apply_k_weighting(self, audio_data: np.ndarray) -> np.ndarray:
+        """professional_meters.py:129-153 (returned as float64 like scipy's filtfilt)."""
+        w, _ = self._eng.weighting(self._frame(audio_data), "K")
+        return w[0].astype(np.float64)
+
+    def apply_weighting(self, audio_data: np.ndarray) -> np.ndarray:
+        """professional_meters.py:220-229: K and Z are implemented on the device."""
+        if self.weighting_mode == "Z" or self.weighting_mode not in ("K", "A", "C"):
+            return audio_data
+        if self.weighting_mode != "K":
+            raise UnsupportedError(-4, f"weighting mode {self.weighting_mode} not implemented")
+        return self.apply_k_weighting(audio_data)
+
+    def calculate_true_peak(self, audio_data: np.ndarray, oversampling: int = 4) -> float:
+        """professional_meters.py:283-299 (float32 result for float32 input, like scipy)."""
+        if len(audio_data) == 0:
+            return -100.0
+        if oversampling != 4:
+            raise UnsupportedError(-4, "only 4x oversampling is implemented")
+        return np.float32(self._eng.true_peak(self._frame(audio_data))[0])
+
+    def calculate_lufs(self, audio_data: np.ndarray) -> Dict[str, float]:
+        """professional_meters.py:231-281."""
+        if len(audio_data) == 0:
+            return self.current_lufs
+        try:
+            x = self._frame(audio_data)
+            mode = "Z" if self.weighting_mode not in ("K", "A", "C") else self.weighting_mode
+            _, li = self._eng.weighting(x, mode, weighted=False)
+            tp = self._eng.true_peak(x)
+            m = self._eng.meter_update(li, tp, 1)[0]
+        except UnsupportedError as e:
+            logger.error(f"calculate_lufs: {e}")
+            return self.current_lufs
+        self.current_lufs["momentary"] = np.float64(m[0])
+        self.current_lufs["short_term"] = np.float64(m[1])
+        self.current_lufs["integrated"] = np.float64(m[2])
+        self.current_lufs["range"] = np.float64(m[3])
+        self.current_lufs["true_peak"] = np.float32(m[4])
+        return self.current_lufs
+
+    def calculate_lufs_batch(self, frames: np.ndarray) -> np.ndarray:
+        """Batched form: frames [F, M] of one stream in order -> [F, 5] dict values per call."""
+        frames = np.ascontiguousarray(frames, dtype=np.float32)
+        _, li = self._eng.weighting(frames, "K", weighted=False)
+        tp = self._eng.true_peak(frames)
+        return self._eng.meter_update(li, tp, frames.shape[0])
+
+    def reset(self):
+        self._eng.reset_meters()
+        self.current_lufs.update({"momentary": -100.0, "short_term": -100.0, "integrated": -100.0, "range": 0.0,
+                                  "true_peak": -100.0})

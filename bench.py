@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: BASELINE cfg2 -- per GPU, 256 stereo frames x 16384 samples (512 channel-frames), the
+full hot path per step: 16k/8k/4k/1k multi-resolution FFT + weighting + combine(512), K-weighted
+LUFS, 4x true peak and the meter aggregates. One process per GPU; frames shard
+across ranks (weak scaling) and each step's per-frame outputs are gathered to rank 0 over RCCL
+(overlapped with the next step). Prints ONE JSON line on rank 0.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "audio-analyzer-omega_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+FS = 48000
+W = 16384
+FRAMES = 256          # stereo frames per GPU (BASELINE cfg2)
+C = 2
+T = 512
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
+PEAK_HBM_GBS = 8000.0
+# SURVEY.md §8(d), per channel-frame (cfg2)
+FLOP_TP = 2.5 * W * np.log2(W) + 2.5 * 4 * W * np.log2(4 * W) + 8 * W          # 3.33 MFLOP (reference algorithm)
+FLOP_FFT = sum(2.5 * n * np.log2(n) + 3.5 * n for n in (16384, 8192, 4096, 1024))  # 1.09 MFLOP
+FLOP_KW = 4 * (W + 18) * 9 + 5 * W                                                 # 0.67 MFLOP
+BYTES_CF = 4 * W + 4 * (T + 2)                                                     # 67,592 B
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cfg2_input(frames=FRAMES, w=W, seed_l=0, seed_r=1):
+    """BASELINE cfg2 synthetic input f32[frames, 2, W]: consecutive frames of
+    L = 0.25 sin(2 pi 440 t) + 0.05 N(0,1), R = 0.25 sin(2 pi 997 t) + 0.05 N(0,1) (seeded). Same formula
+    as oracle/signals.cfg2_batch (checked equal in tests/test_bench_contract.py)."""
+    n = frames * w
+    t = np.arange(n) / FS
+    left = (0.25 * np.sin(2 * np.pi * 440 * t)).astype(np.float32) + \
+        (0.05 * np.random.default_rng(seed_l).standard_normal(n)).astype(np.float32)
+    right = (0.25 * np.sin(2 * np.pi * 997 * t)).astype(np.float32) + \
+        (0.05 * np.random.default_rng(seed_r).standard_normal(n)).astype(np.float32)
+    return np.stack([left.reshape(frames, w), right.reshape(frames, w)], axis=1).astype(np.float32)
+
+
+def kernel_time_ms(eng, xd, reps=20):
+    """Average duration of the dominant kernel (the 8192-point true-peak kernel, one launch per batch)
+    from HIP events on the stream it is launched on (torch's current stream, bound to the context)."""
+    from omega_gpu import _lib as L
+    import ctypes as Cc
+    ncf = xd.numel() // W
+    out = torch.empty(ncf, dtype=torch.float32, device=xd.device)
+    lib = L.lib()
+    eng._bind_stream(xd)
+    for _ in range(3):
+        eng._check(lib.omega_true_peak(eng._ctx, xd.data_ptr(), ncf, W, out.data_ptr(), L.MEM_DEVICE))
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        eng._check(lib.omega_true_peak(eng._ctx, xd.data_ptr(), ncf, W, out.data_ptr(), L.MEM_DEVICE))
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps, ncf
+
+
+def cpu_baseline(seconds):
+    """The oracle (numpy/scipy restatement of the reference path, one core) on the first frames of
+    the same workload until the time budget is spent."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from oracle import omega_ref as R
+    x = cfg2_input(64)
+    st = [R.MeterState(FS), R.MeterState(FS)]
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        f, c = divmod(n, 2)
+        fr = x[f % 64, c]
+        _, _, li, tp = R.full_frame(fr)
+        st[c].update(fr, li, tp)
+        n += 1
+        if time.perf_counter() - t0 > seconds and n >= 8:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "channel-frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} channel-frames of cfg2 (oracle: MRFFT 16k/8k/4k/1k + combine(512) + K-LUFS + "
+                      f"4x TP + meter deques), {dt:.1f} s, OMP_NUM_THREADS=1"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
+
+    # per-rank shard of the cfg2 workload: seeds (2r, 2r+1) per shard
+    x = torch.from_numpy(cfg2_input(FRAMES, W, seed_l=2 * rank, seed_r=2 * rank + 1)).to(dev)
+    eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=T, n_channels=C, device=local)
+    ncf = FRAMES * C
+    bufs = []
+    for _ in range(2):
+        bufs.append({"combined": torch.empty(ncf, T, device=dev), "lufs_inst": torch.empty(ncf, device=dev),
+                     "true_peak_db": torch.empty(ncf, device=dev),
+                     "meters": torch.empty(ncf, 5, dtype=torch.float64, device=dev)})
+    gather = world > 1 and not a.no_gather
+    if gather:
+        import torch.distributed as dist
+        # per-frame output vector: combined[512] + lufs + tp + 5 meters (as float32) = 519 floats
+        packs = [torch.empty(ncf, T + 7, device=dev) for _ in range(2)]
+        recv = [[torch.empty(ncf, T + 7, device=dev) for _ in range(world)] if rank == 0 else None for _ in range(2)]
+        pending = [None, None]
+
+    def step(i):
+        b = i % 2
+        if gather and pending[b] is not None:
+            pending[b].wait()
+        o = eng.process_frames(x, FRAMES, C * W, W, meters=True, out=bufs[b])
+        if gather:
+            p = packs[b]
+            p[:, :T].copy_(o["combined"])
+            p[:, T].copy_(o["lufs_inst"])
+            p[:, T + 1].copy_(o["true_peak_db"])
+            p[:, T + 2:].copy_(o["meters"])
+            pending[b] = dist.gather(p, recv[b], dst=0, async_op=True)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(a.warmup):
+        step(i)
+    if gather:
+        for p in pending:
+            if p is not None:
+                p.wait()
+        pending = [None, None]
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    if gather:
+        for p in pending:
+            if p is not None:
+                p.wait()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    dt = t1 - t0
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    total_cf = ncf * world * a.steps
+    value = total_cf / dt
+
+    kt_ms, kcf = kernel_time_ms(eng, x)
+    flop_launch = FLOP_TP * kcf
+    achieved = flop_launch / (kt_ms * 1e-3) / 1e12
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_baseline(a.cpu_seconds)
+        line = {
+            "metric": "audio frames/sec (multi-res FFT + LUFS + TruePeak) at 1/2/4/8 MI355X",
+            "value": value, "unit": "channel-frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic cfg2 frames (0.25 sine 440/997 Hz + 0.05 N(0,1), seeds per rank)",
+            "config": {"workload": "cfg2: 256 stereo frames x 16384 samples per GPU; MRFFT 16k/8k/4k/1k + "
+                                   "combine(512) + K-weighted LUFS + 4x true peak + meter aggregates",
+                       "channel_frames_per_gpu": ncf, "frame_samples": W, "target_bins": T,
+                       "parallelism": f"frames sharded over {world} GPU(s)" + (", RCCL gather to rank 0" if gather else "")},
+            "roofline": {"bound": "mfma", "kernel": "truepeak_kernel<8192> (4x true peak, fp32)",
+                         "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+                         "kernel_ms": kt_ms, "flop_per_launch": flop_launch,
+                         "note": "fp32 VALU-bound (fp32 MFMA peak = fp32 vector peak); algorithmic flops per "
+                                 "channel-frame from SURVEY.md §8(d) TP formula"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,167 @@
+/*
+ * omega.h -- C ABI of libomega.so, the MI355X (gfx950) engine for the OMEGA-4 per-frame audio
+ * analysis hot path: multi-resolution windowed R2C FFT + psychoacoustic weighting + interpolated
+ * combine, K-weighted LUFS (zero-phase biquads), 4x true peak, the per-stream meter aggregates,
+ * perceptual/mel band reductions and chromagram binning.
+ *
+ * Each entry point replaces one reference Python surface (reference repo paths, file:line):
+ *
+ *   omega_process_frames   MultiResolutionFFT.process_audio_chunk     omega4/audio/multi_resolution_fft.py:228-302
+ *                          + combine_results_optimized                 multi_resolution_fft.py:335-408
+ *                          + ProfessionalMetering.calculate_lufs       omega4/panels/professional_meters.py:231-281
+ *                          (batched over channel-frames; the reference calls these once per display frame,
+ *                           omega4_main.py:707-717 and professional_meters.py:348-351)
+ *   omega_combine          combine_results_optimized                   multi_resolution_fft.py:335-408
+ *   omega_true_peak        ProfessionalMetering.calculate_true_peak    professional_meters.py:283-299
+ *   omega_k_weighting      ProfessionalMetering.apply_k_weighting      professional_meters.py:129-153
+ *                          (+ the instantaneous LUFS of calculate_lufs :236-246)
+ *   omega_meter_*          the momentary/short-term/integrated/range/true-peak deques  professional_meters.py:19-25, :248-279
+ *   omega_bands_*          AudioProcessingPipeline.map_to_bands       omega4/audio/pipeline.py:295-335 (max-reduce)
+ *                          PrecomputedFrequencyMapper.map_spectrum_to_bars omega4/optimization/freq_mapper.py:165-196 (mean-reduce)
+ *   omega_chroma           ChromagramAnalyzer.compute_chromagram      omega4/panels/chromagram.py:109-159
+ *   omega_rfft             BatchedFFTProcessor process_batch (CPU/CuPy branches) omega4/optimization/batched_fft_processor.py:148-285
+ *
+ * Conventions:
+ *   - every function returns 0 on success and a negative omega_status on error; the message is
+ *     available from omega_last_error(ctx). No C++ exception and no abort crosses the ABI.
+ *   - all buffers are caller-owned. `mem` says whether the data pointers are host (OMEGA_MEM_HOST:
+ *     the call stages through context-owned device buffers and returns when outputs are in host
+ *     memory) or device (OMEGA_MEM_DEVICE: the call enqueues on the context stream and returns
+ *     immediately; synchronize with omega_synchronize).
+ *   - one context per host thread (contexts own a HIP stream and the per-channel meter state);
+ *     a context is not internally locked.
+ *   - channel-frame index cf = f * n_channels + c; input sample n of channel-frame (f, c) lives at
+ *     x[f * frame_stride + c * channel_stride + n] (materialized layout: frame_stride = C*W,
+ *     channel_stride = W; stream layout with hop H over planar channels: frame_stride = H,
+ *     channel_stride = samples per channel).
+ */
+#ifndef OMEGA_H
+#define OMEGA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMEGA_ABI_VERSION 1
+#define OMEGA_MAX_RES 4
+#define OMEGA_N_METERS 5 /* momentary, short_term, integrated, range, true_peak */
+
+typedef enum {
+  OMEGA_OK = 0,
+  OMEGA_EINVAL = -1,  /* bad argument / config (the reference raises ValueError) */
+  OMEGA_EHIP = -2,    /* HIP runtime error */
+  OMEGA_ENOMEM = -3,
+  OMEGA_EUNSUP = -4   /* valid for the reference, not supported by this build (e.g. non power-of-2 M) */
+} omega_status;
+
+typedef enum { OMEGA_MEM_HOST = 0, OMEGA_MEM_DEVICE = 1 } omega_mem;
+
+typedef enum {
+  OMEGA_WIN_BLACKMAN = 0, /* np.blackman, multi_resolution_fft.py:177-178 */
+  OMEGA_WIN_HANN = 1,     /* np.hanning, batched_fft_processor.py:94 */
+  OMEGA_WIN_HAMMING = 2,  /* np.hamming */
+  OMEGA_WIN_RECT = 3      /* ones */
+} omega_window;
+
+/* One FFT resolution: FFTConfig (multi_resolution_fft.py:26-44). */
+typedef struct {
+  double freq_lo, freq_hi; /* inclusive range [lo, hi] in Hz */
+  int32_t fft_size;        /* power of two, 512..16384, <= frame_size */
+  int32_t hop_size;        /* kept for fidelity (CircularBuffer sizing); the frame API is stateless */
+  double weight;           /* base psychoacoustic weight and combine weight */
+  int32_t window;          /* omega_window */
+} omega_resolution;
+
+typedef struct {
+  int32_t sample_rate;     /* fs */
+  double max_freq;         /* combine grid top: min(max_freq, fs/2) (multi_resolution_fft.py:146) */
+  int32_t n_res;           /* 1..OMEGA_MAX_RES */
+  omega_resolution res[OMEGA_MAX_RES];
+  int32_t apply_weighting; /* process_audio_chunk(apply_weighting=...) */
+  int32_t target_bins;     /* T of combine_results_optimized, 2..4096 */
+  int32_t frame_size;      /* W = metering window M: power of two 512..16384 */
+  int32_t n_channels;      /* independent streams; one meter state each */
+  double gate_lufs;        /* -70 (professional_meters.py:36) */
+  int32_t momentary_len, short_len, integrated_len, peak_len; /* 24, 180, 3600, 60 (:20-25) */
+} omega_config;
+
+/* Per-call outputs; any pointer may be NULL to skip that stage. */
+typedef struct {
+  float* combined;              /* [n_cf, T] combine_results_optimized magnitude */
+  float* lufs_inst;             /* [n_cf] instantaneous K-weighted LUFS (-100 when silent) */
+  float* true_peak_db;          /* [n_cf] calculate_true_peak (dBTP, -100 when silent) */
+  double* meters;               /* [n_cf, 5] calculate_lufs dict values; advances the meter state */
+  float* mag[OMEGA_MAX_RES];    /* [n_cf, N_r/2+1] weighted magnitude per resolution (full-magnitude mode) */
+  float* weighted;              /* [n_cf, W] K-weighted signal (apply_k_weighting) */
+} omega_outputs;
+
+typedef struct omega_ctx omega_ctx;
+
+/* Reference defaults: the four resolutions of multi_resolution_fft.py:149-154, fs 48000,
+ * max_freq 20000, T 1024, W 4096, one channel, gate/deques of professional_meters.py:20-36. */
+void omega_config_default(omega_config* cfg);
+
+int omega_create(const omega_config* cfg, int device, omega_ctx** out);
+void omega_destroy(omega_ctx* ctx);
+const char* omega_last_error(const omega_ctx* ctx);
+const char* omega_version(void);
+/* Use a caller-owned hipStream_t (NULL restores the context's own stream). */
+int omega_set_stream(omega_ctx* ctx, void* hip_stream);
+int omega_synchronize(omega_ctx* ctx);
+
+/* The fused per-channel-frame hot path over n_frames x n_channels frames of W samples. */
+int omega_process_frames(omega_ctx* ctx, const float* x, int64_t n_frames, int64_t frame_stride,
+                         int64_t channel_stride, const omega_outputs* out, int mem);
+
+/* combine_results_optimized over externally supplied weighted magnitudes; mags[r] may be NULL
+ * (resolution absent from the results dict). out: [n_cf, T]. */
+int omega_combine(omega_ctx* ctx, const float* const* mags, int64_t n_cf, float* out, int mem);
+
+/* calculate_true_peak(x, 4) for n frames of length m (power of two 512..16384), contiguous. */
+int omega_true_peak(omega_ctx* ctx, const float* x, int64_t n, int32_t m, float* out_db, int mem);
+
+/* apply_k_weighting for n frames of length m (power of two 512..16384): weighted [n, m] (may be
+ * NULL) and the instantaneous LUFS [n] (may be NULL). */
+int omega_k_weighting(omega_ctx* ctx, const float* x, int64_t n, int32_t m, float* weighted,
+                      float* lufs_inst, int mem);
+
+/* apply_weighting + instantaneous LUFS for a weighting mode (professional_meters.py:220-229):
+ * K (0) and Z (3: the signal itself, no gate) are implemented; A (1) and C (2) return OMEGA_EUNSUP. */
+typedef enum { OMEGA_WEIGHT_K = 0, OMEGA_WEIGHT_A = 1, OMEGA_WEIGHT_C = 2, OMEGA_WEIGHT_Z = 3 } omega_weighting_mode;
+int omega_weighting(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t mode, float* weighted,
+                    float* lufs_inst, int mem);
+
+/* Meter aggregates from precomputed instantaneous values: feeds n_frames x n_channels values
+ * (cf-major) through the per-channel state and writes meters [n_cf, 5]. */
+int omega_meter_update(omega_ctx* ctx, const float* lufs_inst, const float* tp_db, int64_t n_frames,
+                       double* meters, int mem);
+int omega_meter_reset(omega_ctx* ctx);
+
+/* ---- band reductions (A10/A11) ---- */
+typedef struct omega_bands omega_bands;
+typedef enum { OMEGA_BANDS_MAX = 0, OMEGA_BANDS_MEAN = 1 } omega_band_op;
+/* n_bands bands [starts[i], ends[i]) over spectra of n_bins bins. MAX: out[i] = max(spec[s:e]) *
+ * scale[i] (pipeline.py:313-324); MEAN: out[i] = mean((spec*bin_scale)[s:e]) (freq_mapper.py:180-194).
+ * scale / bin_scale may be NULL (ones). Bands whose end exceeds n_bins are 0 (MAX) or stop the
+ * table (MEAN, freq_mapper.py:188-189), exactly as the reference. */
+int omega_bands_create(omega_ctx* ctx, int op, const int32_t* starts, const int32_t* ends,
+                       int32_t n_bands, int32_t n_out, const double* scale, const double* bin_scale,
+                       int32_t n_bins, omega_bands** out);
+void omega_bands_destroy(omega_bands* b);
+int omega_bands_apply(omega_ctx* ctx, omega_bands* b, const float* spec, int64_t n, int64_t spec_stride,
+                      float* out, int mem);
+
+/* ---- chromagram (A12) over n spectra of n_bins bins with uniform rfftfreq spacing df ---- */
+int omega_chroma(omega_ctx* ctx, const float* spec, int64_t n, int32_t n_bins, double df,
+                 double* out_raw, int mem);
+
+/* ---- windowed R2C FFT (A13): magnitude [n, m/2+1] and/or complex [n, m/2+1] (interleaved) ---- */
+int omega_rfft(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t window, float* mag,
+               float* cplx, int mem);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OMEGA_H */

@@ -1,0 +1,327 @@
+"""Parity of the HIP path (through the C ABI, via the omega_gpu facades) against the reference's golden
+vectors and the oracle. Tolerances are the north-star bars (BASELINE.json): spectra <= 1e-4 normwise
+(|a-b|_inf / max|b| per frame and resolution), LUFS <= 0.1 LU; true peak <= 0.01 dB."""
+import numpy as np
+import pytest
+
+from conftest import load_golden, normwise
+from oracle import omega_ref as R
+from oracle import signals as S
+
+pytestmark = pytest.mark.gpu
+FS = 48000
+SPEC_TOL = 1e-4   # north star: <= 1e-4 relative on float32 spectra (normwise)
+LU_TOL = 0.1      # north star: <= 0.1 LU on LUFS
+TP_TOL_DB = 0.01  # true peak (float32 FFT on both sides)
+
+
+@pytest.fixture(scope="module")
+def mr():
+    return load_golden("mrfft")
+
+
+@pytest.fixture(scope="module")
+def me():
+    return load_golden("meters")
+
+
+def _mrfft(configs=None):
+    from omega_gpu.multi_resolution_fft import MultiResolutionFFT, FFTConfig
+    m = MultiResolutionFFT(FS)
+    if configs is not None:
+        m.configs = [FFTConfig(*c) for c in configs]
+        m._setup_windows(); m._setup_buffers(); m._setup_frequency_arrays(); m._setup_working_arrays()
+    return m
+
+
+NS = [((20, 200), 16384, 1024, 1.5), ((200, 1000), 8192, 512, 1.2), ((1000, 5000), 4096, 256, 1.0),
+      ((5000, 20000), 1024, 256, 1.5)]
+
+
+def test_native_library_is_the_path():
+    import omega_gpu
+    assert omega_gpu.lib().omega_version().startswith(b"omega-mi355x")
+
+
+@pytest.mark.parametrize("name", ["sine1k_2048", "noise_2048", "triad_4096", "comp_4096", "silence_4096",
+                                  "sine50_8192"])
+def test_mrfft_golden_default(mr, name):
+    m = _mrfft()
+    x = mr[f"{name}/x"]
+    res = m.process_audio_chunk(x)
+    assert sorted(res) == list(mr[f"{name}/res"])
+    for i, r in res.items():
+        assert r.magnitude.dtype == np.float32 and r.config_index == i
+        g = mr[f"{name}/mag{i}"]
+        if np.max(g) == 0:
+            assert np.max(np.abs(r.magnitude)) == 0
+        else:
+            assert normwise(r.magnitude, g) < SPEC_TOL, (i, normwise(r.magnitude, g))
+        np.testing.assert_array_equal(r.frequencies, np.fft.rfftfreq(m.configs[i].fft_size, 1 / FS))
+    raw = _mrfft().process_audio_chunk(x, apply_weighting=False)
+    for i, r in raw.items():
+        g = mr[f"{name}/raw{i}"]
+        if np.max(g) > 0:
+            assert normwise(r.magnitude, g) < SPEC_TOL
+    for T in (512, 1024):
+        c, t = m.combine_results_optimized(res, target_bins=T)
+        np.testing.assert_array_equal(t, mr[f"{name}/tgt{T}"])
+        g = mr[f"{name}/comb{T}"]
+        assert c.dtype == np.float32 and c.shape == (T,)
+        assert (np.max(np.abs(c)) == 0) if np.max(g) == 0 else normwise(c, g) < SPEC_TOL
+
+
+@pytest.mark.parametrize("k", [0, 1, 2])
+def test_mrfft_golden_northstar(mr, k):
+    m = _mrfft(NS)
+    res = m.process_audio_chunk(mr[f"ns{k}/x"])
+    assert sorted(res) == [0, 1, 2, 3]
+    for i in range(4):
+        assert normwise(res[i].magnitude, mr[f"ns{k}/mag{i}"]) < SPEC_TOL
+    c, _ = m.combine_results_optimized(res, 512)
+    assert normwise(c, mr[f"ns{k}/comb512"]) < SPEC_TOL
+
+
+def test_mrfft_stream_layout(mr):
+    """One instance fed 512-sample chunks: CircularBuffer availability and contents."""
+    m = _mrfft()
+    x = mr["stream/x"]
+    for c in range(24):
+        r = m.process_audio_chunk(x[c * 512:(c + 1) * 512])
+        assert sum(1 << i for i in r) == mr["stream/resmask"][c]
+        comb = m.combine_results_optimized(r, 512)[0] if r else np.zeros(512, np.float32)
+        g = mr["stream/comb512"][c]
+        assert (np.max(np.abs(comb)) == 0) if np.max(g) == 0 else normwise(comb, g) < SPEC_TOL
+    for i in r:
+        assert normwise(r[i].magnitude, mr[f"stream/mag{i}"]) < SPEC_TOL
+
+
+def test_mrfft_empty_chunk():
+    m = _mrfft()
+    assert m.process_audio_chunk(np.zeros(0, np.float32)) == {}
+    z, t = m.combine_results_optimized({}, 512)
+    assert z.shape == (512,) and not z.any() and t[-1] == 20000
+
+
+@pytest.mark.parametrize("name", ["sine2048", "hann2048_f64"])
+def test_k_weighting_golden(me, name):
+    from omega_gpu.professional_meters import ProfessionalMetering
+    pm = ProfessionalMetering(FS)
+    x = me[f"kw/{name}/x"]
+    y = pm.apply_k_weighting(x)
+    g = me[f"kw/{name}/y"]
+    assert y.dtype == np.float64
+    assert normwise(y, g) < SPEC_TOL
+    ms_dev, ms_ref = np.mean(y ** 2), np.mean(g ** 2)
+    assert abs(10 * np.log10(ms_dev) - 10 * np.log10(ms_ref)) < LU_TOL
+    assert abs(pm.calculate_true_peak(x) - me[f"kw/{name}/tp"]) < TP_TOL_DB
+
+
+def test_k_weighting_coefficients(me):
+    from omega_gpu.professional_meters import ProfessionalMetering
+    kf = ProfessionalMetering(FS).k_weighting_filter
+    for k, g in (("hp_b", "coef/hp_b"), ("hp_a", "coef/hp_a"), ("shelf_b", "coef/sh_b"), ("shelf_a", "coef/sh_a")):
+        np.testing.assert_allclose(kf[k], me[g], rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("name", ["cfg2L", "sine2048", "low50_4096", "silence", "steps1024", "square1024"])
+def test_meter_sequences_facade(me, name):
+    """calculate_lufs called frame by frame (the panel's call pattern, professional_meters.py:348-351)."""
+    from omega_gpu.professional_meters import ProfessionalMetering
+    pm = ProfessionalMetering(FS)
+    frames = me[f"{name}/x"]
+    agg = me[f"{name}/agg"]
+    for f, x in enumerate(frames):
+        d = pm.calculate_lufs(x)
+        assert set(d) == {"momentary", "short_term", "integrated", "range", "true_peak"}
+        got = np.array([d[k] for k in ("momentary", "short_term", "integrated", "range", "true_peak")])
+        assert np.all(np.abs(got[:4] - agg[f, :4]) < LU_TOL), (f, got, agg[f])
+        assert abs(got[4] - agg[f, 4]) < TP_TOL_DB, (f, got[4], agg[f, 4])
+    assert d is pm.current_lufs
+
+
+@pytest.mark.parametrize("name", ["cfg2L", "sine2048", "steps1024"])
+def test_meter_instantaneous(me, name):
+    from omega_gpu import Engine, Resolution
+    frames = me[f"{name}/x"]
+    e = Engine([Resolution((20, 20000), 512, 256, 1.0)], FS, 20000, 2, frame_size=512)
+    _, li = e.k_weighting(frames, weighted=False)
+    np.testing.assert_allclose(li, me[f"{name}/lufs_inst"], rtol=0, atol=LU_TOL)
+    tp = e.true_peak(frames)
+    np.testing.assert_allclose(tp, me[f"{name}/tp"], rtol=0, atol=TP_TOL_DB)
+    # record how close the float32 scan IIR actually is (well inside the 0.1 LU bar)
+    assert np.max(np.abs(li - me[f"{name}/lufs_inst"])) < 0.01
+
+
+def test_meter_long_window_batch(me):
+    """3700 frames: the 3600-deep integrated window evicts; batched form on the device."""
+    from omega_gpu.professional_meters import ProfessionalMetering
+    pm = ProfessionalMetering(FS)
+    out = pm.calculate_lufs_batch(S.level_steps(3700, 512, seed=9))
+    g = me["long/agg"]
+    assert np.max(np.abs(out[:, :4] - g[:, :4])) < LU_TOL
+    assert np.max(np.abs(out[:, 4] - g[:, 4])) < TP_TOL_DB
+
+
+def test_meter_aggregates_exact_on_injected_values(me):
+    """A9 in isolation: with the oracle's instantaneous values (rounded to float32, as the device
+    stores them) the aggregates -- means, gated mean, numpy-'linear' percentiles, peak hold -- match a
+    float64 restatement to 1e-9, across batch boundaries (state carried between calls)."""
+    from omega_gpu import Engine, Resolution
+    li = me["long/lufs_inst"].astype(np.float32)
+    tp = me["long/tp"].astype(np.float32)
+    e = Engine([Resolution((20, 20000), 512, 256, 1.0)], FS, 20000, 2, frame_size=512)
+    outs = [e.meter_update(li[a:b], tp[a:b], b - a) for a, b in ((0, 1), (1, 700), (700, 3650), (3650, 3700))]
+    dev = np.concatenate(outs)
+    st = R.MeterState(FS)
+    ref = np.array([[v for v in st.update(np.ones(1), float(li[f]), float(tp[f])).values()] for f in range(3700)])
+    np.testing.assert_allclose(dev, ref, rtol=0, atol=1e-9)
+
+
+def test_batched_frames_match_facade(me):
+    """The fused batch path (process_frames with meters) equals frame-by-frame calculate_lufs."""
+    from omega_gpu import Engine, Resolution
+    frames = me["sine2048/x"]
+    e = Engine([Resolution((20, 200), 2048, 512, 1.5)], FS, 20000, 64, n_channels=1)
+    out = e.process_frames(frames.ravel(), len(frames), 2048, 2048, combined=False, meters=True)
+    g = me["sine2048/agg"]
+    assert np.max(np.abs(out["meters"][:, :4] - g[:, :4])) < LU_TOL
+    assert np.max(np.abs(out["meters"][:, 4] - g[:, 4])) < TP_TOL_DB
+
+
+def test_meter_unsupported_length_keeps_state():
+    from omega_gpu.professional_meters import ProfessionalMetering
+    pm = ProfessionalMetering(FS)
+    before = dict(pm.calculate_lufs(S.sine(1000, 0.1, 2048)))
+    after = pm.calculate_lufs(S.sine(1000, 0.1, 480))  # reference-valid, not a power of two here
+    assert after == before
+    assert pm.calculate_lufs(np.zeros(0, np.float32)) is pm.current_lufs
+
+
+def test_bands_golden(golden):
+    from omega_gpu.bands import PipelineBands, PrecomputedFrequencyMapper
+    g = golden("bands")
+    mags = g["mags8192"]
+    for nb, fft in ((512, 8192), (768, 4096)):
+        pb = PipelineBands(FS, nb, fft)
+        np.testing.assert_array_equal(pb.starts, g[f"pipe{nb}_{fft}/starts"])
+        np.testing.assert_array_equal(pb.ends, g[f"pipe{nb}_{fft}/ends"])
+        src = mags if fft == 8192 else mags[:, : fft // 2 + 1]
+        out = np.stack([pb.map_to_bands(m, apply_smoothing=False) for m in src])
+        np.testing.assert_allclose(out, g[f"pipe{nb}_{fft}/out"], rtol=1e-6)
+        sm = np.stack([pb.map_to_bands(m, apply_smoothing=True) for m in src])
+        np.testing.assert_allclose(sm, g[f"pipe{nb}_{fft}/smooth"], rtol=1e-6)
+    for fft, nb in ((2048, 512), (8192, 512)):
+        fm = PrecomputedFrequencyMapper(FS, fft, nb)
+        np.testing.assert_array_equal(np.array(fm.band_indices), g[f"mel{fft}_{nb}/bands"])
+        spec = g[f"mel{fft}_{nb}/spec"]
+        np.testing.assert_allclose(np.stack([fm.map_spectrum_to_bars(s, True) for s in spec]),
+                                   g[f"mel{fft}_{nb}/out_comp"], rtol=1e-5)
+        np.testing.assert_allclose(np.stack([fm.map_spectrum_to_bars(s, False) for s in spec]),
+                                   g[f"mel{fft}_{nb}/out_raw"], rtol=1e-5)
+        np.testing.assert_allclose(np.stack([fm.map_spectrum_to_bars(s[:512], False) for s in spec]),
+                                   g[f"mel{fft}_{nb}/out_512in"], rtol=1e-5)
+
+
+def test_chroma_golden(golden):
+    from omega_gpu.chromagram import ChromagramAnalyzer
+    g = golden("chroma")
+    ca = ChromagramAnalyzer(FS)
+    out = np.stack([ca.compute_chromagram(m, g["freqs"]) for m in g["mags"]])
+    np.testing.assert_allclose(out, g["out"], rtol=1e-6, atol=1e-9)
+    a = ChromagramAnalyzer(FS).compute_chromagram(g["a440_mag"], g["freqs"])
+    assert int(np.argmax(a)) == 9
+    np.testing.assert_allclose(a, g["a440_out"], rtol=1e-6, atol=1e-9)
+
+
+def test_batched_fft_golden(golden):
+    from omega_gpu.batched_fft_processor import BatchedFFTProcessor
+    g = golden("batched")
+    bp = BatchedFFTProcessor()
+    cases = (("app_f64_2048_hann", 2048, "hann"), ("f32_4096_blackman", 4096, "blackman"),
+             ("pad_1000_1024_hamming", 1024, "hamming"), ("trim_20000_16384_hann", 16384, "hann"))
+    ids = {name: bp.prepare_batch(name, g[f"{name}/x"], n, w) for name, n, w in cases}
+    assert bp.process_batch() == 4
+    res = bp.distribute_results()
+    for name, n, w in cases:
+        r = res[ids[name]]
+        assert normwise(r["magnitude"], g[f"{name}/mag"]) < SPEC_TOL
+        assert normwise(np.abs(r["complex"] - g[f"{name}/complex"]), np.abs(g[f"{name}/complex"])) < SPEC_TOL
+
+
+# ---- BASELINE cfg2 at full size: size-independent properties + sampled oracle parity ----
+
+@pytest.fixture(scope="module")
+def cfg2():
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    x = S.cfg2_batch(256)
+    eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+    xd = torch.from_numpy(x).cuda()
+    out = eng.process_frames(xd, 256, 2 * 16384, 16384, meters=True)
+    torch.cuda.synchronize()
+    return x, eng, xd, {k: v.cpu().numpy() for k, v in out.items()}
+
+
+def test_cfg2_sampled_frames_match_oracle(cfg2):
+    x, _, _, out = cfg2
+    for f, c in ((0, 0), (7, 1), (128, 0), (255, 1)):
+        res, comb, li, tp = R.full_frame(x[f, c])
+        cf = f * 2 + c
+        assert normwise(out["combined"][cf], comb) < SPEC_TOL
+        assert abs(out["lufs_inst"][cf] - li) < LU_TOL
+        assert abs(out["true_peak_db"][cf] - tp) < TP_TOL_DB
+
+
+def test_cfg2_properties(cfg2):
+    import torch
+    x, eng, xd, out = cfg2
+    assert np.isfinite(out["combined"]).all() and (out["combined"] >= 0).all()
+    peak_db = 20 * np.log10(np.abs(x).max(axis=2)).reshape(-1)
+    assert (out["true_peak_db"] >= peak_db - 1e-4).all()  # true peak >= sample peak
+    # linearity: 2x input -> 2x spectrum, +6.02 dB LUFS and true peak
+    eng.reset_meters()
+    o2 = eng.process_frames(xd * 2, 256, 2 * 16384, 16384)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(o2["combined"].cpu().numpy(), 2 * out["combined"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(o2["lufs_inst"].cpu().numpy() - out["lufs_inst"], 20 * np.log10(2), atol=1e-3)
+    np.testing.assert_allclose(o2["true_peak_db"].cpu().numpy() - out["true_peak_db"], 20 * np.log10(2), atol=1e-3)
+    # determinism: the same launch twice is bitwise identical
+    o3 = eng.process_frames(xd * 2, 256, 2 * 16384, 16384)
+    torch.cuda.synchronize()
+    for k in ("combined", "lufs_inst", "true_peak_db"):
+        assert torch.equal(o2[k], o3[k])
+
+
+def test_cfg2_meter_state_matches_oracle_sequence(cfg2):
+    """meters[f, c] after the batch equal 256 sequential calculate_lufs calls per channel."""
+    x, _, _, out = cfg2
+    li = out["lufs_inst"].reshape(256, 2)
+    tp = out["true_peak_db"].reshape(256, 2)
+    for c in (0, 1):
+        st = R.MeterState(FS)
+        ref = np.array([list(st.update(np.ones(1), float(li[f, c]), float(tp[f, c])).values()) for f in range(256)])
+        np.testing.assert_allclose(out["meters"].reshape(256, 2, 5)[:, c], ref, rtol=0, atol=1e-9)
+
+
+def test_stream_layout_hop(cfg2):
+    """Stream layout: overlapping frames of one planar stream via frame_stride = hop."""
+    import torch
+    from omega_gpu import Engine, Resolution
+    W, H, F = 4096, 1024, 16
+    s = S.sine(440, 0.25, W + H * (F - 1)) + S.noise(3, W + H * (F - 1), 0.05)
+    eng = Engine([Resolution((20, 20000), 4096, 1024, 1.0)], FS, 20000, 256)
+    out = eng.process_frames(s, F, H, 0, combined=True, true_peak=True)
+    for f in (0, 5, 15):
+        fr = s[f * H:f * H + W]
+        res = R.mrfft_frame(fr, [R.FFTConfig((20, 20000), 4096, 1024, 1.0)], FS)
+        comb, _ = R.combine(res, [R.FFTConfig((20, 20000), 4096, 1024, 1.0)], FS, 20000, 256)
+        assert normwise(out["combined"][f], comb) < SPEC_TOL
+        assert abs(out["true_peak_db"][f] - R.true_peak(fr)) < TP_TOL_DB
+
+
+def test_zero_frames_is_noop():
+    from omega_gpu import Engine, Resolution
+    e = Engine([Resolution((20, 20000), 1024, 256, 1.0)], FS, 20000, 16)
+    out = e.process_frames(np.zeros(1024, np.float32), 0, 1024, 1024)
+    assert out["combined"].shape == (0, 16)
