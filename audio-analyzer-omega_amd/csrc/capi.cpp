@@ -22,9 +22,12 @@
 
 namespace omega {
 hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s);
+hipError_t launch_mrfft(const SpectralParams& p, hipStream_t s);
+hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
-hipError_t launch_meters(const MeterParams& p, const MeterStateParams& sp, hipStream_t s);
+hipError_t launch_meters(const MeterParams& p, const MeterStateParams& sp, unsigned long long* sorted, int* n_sorted,
+                         hipStream_t s);
 hipError_t launch_bands(const BandParams& p, hipStream_t s);
 hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int hi, const double* mat, double* out,
                          hipStream_t s);
@@ -36,6 +39,7 @@ using namespace omega;
 namespace {
 
 constexpr double kPi = 3.14159265358979323846;
+constexpr int kSortCapHost = 8192;  // meters.hip kSortCap
 
 struct DevBuf {
   void* p = nullptr;
@@ -141,6 +145,16 @@ struct omega_ctx {
   omega_config cfg{};
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
+  // fork/join streams + events for the concurrent branches, and the graph cache
+  hipStream_t cap = nullptr, fork[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+  bool use_graph = true;
+  struct GraphEntry {
+    std::vector<uint64_t> key;
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+  };
+  std::vector<GraphEntry> graphs;
   std::string err;
   // tables
   float2* d_tw[kMaxLog2] = {};
@@ -167,6 +181,8 @@ struct omega_ctx {
   int* d_nl[2] = {};
   int* d_nt[2] = {};
   int cur = 0;
+  unsigned long long* d_sorted = nullptr;  // [C, 8192] gated union keys (meter_sort_kernel scratch)
+  int* d_nsorted = nullptr;
   int HL = 0, HT = 0;
   // staging for OMEGA_MEM_HOST
   std::vector<DevBuf> stage;
@@ -315,8 +331,8 @@ int validate(omega_ctx* c, const omega_config* cfg) {
   }
   if (cfg->target_bins < 1 || cfg->target_bins > (1 << 24)) return fail(c, OMEGA_EINVAL, "target_bins out of range");
   if (cfg->n_channels < 1) return fail(c, OMEGA_EINVAL, "n_channels must be >= 1");
-  if (cfg->integrated_len < 1 || cfg->integrated_len > 57 * 64)
-    return fail(c, OMEGA_EUNSUP, "integrated_len %d: 1..3648 supported", cfg->integrated_len);
+  if (cfg->integrated_len < 1 || cfg->integrated_len > 4096)
+    return fail(c, OMEGA_EUNSUP, "integrated_len %d: 1..4096 supported", cfg->integrated_len);
   if (cfg->momentary_len < 1 || cfg->short_len < 1 || cfg->peak_len < 1)
     return fail(c, OMEGA_EINVAL, "deque lengths must be >= 1");
   return 0;
@@ -455,6 +471,9 @@ int build_meter_state(omega_ctx* c) {
     if (!e) e = dalloc(c, &c->d_nt[b], C);
     if (e) return e;
   }
+  int e = dalloc(c, &c->d_sorted, (size_t)C * kSortCapHost);
+  if (!e) e = dalloc(c, &c->d_nsorted, C);
+  if (e) return e;
   return omega_meter_reset(c);
 }
 
@@ -520,42 +539,74 @@ int finish_host(omega_ctx* c, const std::vector<HostOut>& outs) {
   return 0;
 }
 
-int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_frames, double* out) {
-  MeterParams p{};
-  p.lufs = lufs;
-  p.tp = tp;
-  p.n_frames = n_frames;
-  p.C = c->cfg.n_channels;
-  p.hist_l = c->d_hist_l[c->cur];
-  p.hist_t = c->d_hist_t[c->cur];
-  p.n_hist_l = c->d_nl[c->cur];
-  p.n_hist_t = c->d_nt[c->cur];
-  p.HL = c->HL;
-  p.HT = c->HT;
-  p.mom_len = c->cfg.momentary_len;
-  p.short_len = c->cfg.short_len;
-  p.int_len = c->cfg.integrated_len;
-  p.peak_len = c->cfg.peak_len;
-  p.gate = (float)c->cfg.gate_lufs;
-  p.out = out;
-  MeterStateParams s{};
-  s.lufs = lufs;
-  s.tp = tp;
-  s.n_frames = n_frames;
-  s.C = p.C;
-  s.hist_l_in = p.hist_l;
-  s.hist_t_in = p.hist_t;
-  s.n_l_in = p.n_hist_l;
-  s.n_t_in = p.n_hist_t;
-  const int nx = c->cur ^ 1;
-  s.hist_l_out = c->d_hist_l[nx];
-  s.hist_t_out = c->d_hist_t[nx];
-  s.n_l_out = c->d_nl[nx];
-  s.n_t_out = c->d_nt[nx];
-  s.HL = c->HL;
-  s.HT = c->HT;
-  HIPC(c, launch_meters(p, s, c->stream));
-  c->cur = nx;
+// The sorted-union scratch holds (integrated_len - 1) history values plus one chunk of frames.
+int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_frames, double* out,
+                   hipStream_t stream) {
+  const int C = c->cfg.n_channels;
+  const int64_t chunk = std::min<int64_t>(4096, kSortCapHost - c->HL);
+  for (int64_t f0 = 0; f0 < n_frames; f0 += chunk) {
+    const int64_t nf = std::min(chunk, n_frames - f0);
+    MeterParams p{};
+    p.lufs = lufs + f0 * C;
+    p.tp = tp + f0 * C;
+    p.n_frames = nf;
+    p.C = C;
+    p.hist_l = c->d_hist_l[c->cur];
+    p.hist_t = c->d_hist_t[c->cur];
+    p.n_hist_l = c->d_nl[c->cur];
+    p.n_hist_t = c->d_nt[c->cur];
+    p.HL = c->HL;
+    p.HT = c->HT;
+    p.mom_len = c->cfg.momentary_len;
+    p.short_len = c->cfg.short_len;
+    p.int_len = c->cfg.integrated_len;
+    p.peak_len = c->cfg.peak_len;
+    p.gate = (float)c->cfg.gate_lufs;
+    p.out = out + f0 * C * OMEGA_N_METERS;
+    MeterStateParams s{};
+    s.lufs = p.lufs;
+    s.tp = p.tp;
+    s.n_frames = nf;
+    s.C = C;
+    s.hist_l_in = p.hist_l;
+    s.hist_t_in = p.hist_t;
+    s.n_l_in = p.n_hist_l;
+    s.n_t_in = p.n_hist_t;
+    const int nx = c->cur ^ 1;
+    s.hist_l_out = c->d_hist_l[nx];
+    s.hist_t_out = c->d_hist_t[nx];
+    s.n_l_out = c->d_nl[nx];
+    s.n_t_out = c->d_nt[nx];
+    s.HL = c->HL;
+    s.HT = c->HT;
+    HIPC(c, launch_meters(p, s, c->d_sorted, c->d_nsorted, stream));
+    c->cur = nx;
+  }
+  return 0;
+}
+
+// The per-batch work as three branches forked from `s` and joined back on it:
+//   s:        multi-resolution kernels (resolution order)
+//   fork[0]:  true peak          fork[1]: K-weighting + LUFS
+//   s:        meter aggregates (after the join: they need LUFS and true peak)
+int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, int64_t n_frames,
+                   const float* lufs, const float* tp, double* meters, hipStream_t s) {
+  const bool do_tp = sp.tp_out != nullptr, do_kw = kp.lufs_out || kp.weighted_out;
+  HIPC(c, hipEventRecord(c->ev_fork, s));
+  if (do_tp) {
+    HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
+    HIPC(c, launch_truepeak(W, sp, c->fork[0]));
+    HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
+  }
+  if (do_kw) {
+    HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_fork, 0));
+    HIPC(c, launch_kweight(W, kp, c->fork[1]));
+    HIPC(c, hipEventRecord(c->ev_join[1], c->fork[1]));
+  }
+  HIPC(c, launch_mrfft(sp, s));
+  if (do_tp) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
+  if (do_kw) HIPC(c, hipStreamWaitEvent(s, c->ev_join[1], 0));
+  if (meters) return meters_enqueue(c, lufs, tp, n_frames, meters, s);
   return 0;
 }
 
@@ -606,6 +657,16 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
     return fail(c, OMEGA_EHIP, "device %d: %s", device, hipGetErrorString(he));
   }
   c->stream = c->own;
+  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking);
+  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->fork[0], hipStreamNonBlocking);
+  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->fork[1], hipStreamNonBlocking);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_join[0], hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_join[1], hipEventDisableTiming);
+  if (he != hipSuccess) {
+    *out = c;
+    return fail(c, OMEGA_EHIP, "streams/events: %s", hipGetErrorString(he));
+  }
   e = build_twiddles(c);
   if (!e) e = build_spectral_tables(c);
   if (!e) e = build_meter_state(c);
@@ -621,6 +682,14 @@ void omega_destroy(omega_ctx* c) {
   for (auto& kv : c->chroma_mats) (void)hipFree(kv.second.first);
   for (DevBuf& b : c->stage)
     if (b.p) (void)hipFree(b.p);
+  for (auto& g : c->graphs) {
+    (void)hipGraphExecDestroy(g.exec);
+    (void)hipGraphDestroy(g.graph);
+  }
+  for (hipStream_t st : {c->cap, c->fork[0], c->fork[1]})
+    if (st) (void)hipStreamDestroy(st);
+  for (hipEvent_t ev : {c->ev_fork, c->ev_join[0], c->ev_join[1]})
+    if (ev) (void)hipEventDestroy(ev);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
@@ -629,7 +698,13 @@ const char* omega_last_error(const omega_ctx* c) { return c ? c->err.c_str() : "
 
 int omega_set_stream(omega_ctx* c, void* s) {
   if (!c) return OMEGA_EINVAL;
-  c->stream = s ? static_cast<hipStream_t>(s) : c->own;
+  c->stream = static_cast<hipStream_t>(s);  // NULL = the null (default) stream, e.g. torch's default
+  return 0;
+}
+
+int omega_set_graphs(omega_ctx* c, int enable) {
+  if (!c) return OMEGA_EINVAL;
+  c->use_graph = enable != 0;
   return 0;
 }
 
@@ -702,18 +777,51 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
   sp.comb_out = comb;
   sp.tp_out = tp;
   for (int r = 0; r < c->cfg.n_res; ++r) sp.res[r].mag_out = mags[r];
-  HIPC(c, launch_spectral(W, sp, c->stream));
+  BiquadTab* tabs = nullptr;
   if (lufs || weighted) {
-    BiquadTab* tabs = nullptr;
     e = get_kw_tab(c, W, &tabs);
     if (e) return e;
-    KWeightParams kp{dx, frame_stride, channel_stride, C, ncf, tabs, tabs + 1, lufs, weighted, 0};
-    HIPC(c, launch_kweight(W, kp, c->stream));
   }
-  if (meters) {
-    e = meters_enqueue(c, lufs, tp, n_frames, meters);
-    if (e) return e;
+  KWeightParams kp{dx, frame_stride, channel_stride, C, ncf, tabs, tabs ? tabs + 1 : nullptr, lufs, weighted, 0};
+  if (mem == OMEGA_MEM_DEVICE && c->use_graph) {
+    // replay a captured graph of this exact call (pointers, sizes, meter-state parity), capturing it on
+    // first use: removes the per-launch host cost and runs the three branches concurrently
+    const std::vector<uint64_t> key = {(uint64_t)dx, (uint64_t)n_frames, (uint64_t)frame_stride,
+                                       (uint64_t)channel_stride, (uint64_t)comb, (uint64_t)lufs, (uint64_t)tp,
+                                       (uint64_t)meters, (uint64_t)weighted, (uint64_t)mags[0], (uint64_t)mags[1],
+                                       (uint64_t)mags[2], (uint64_t)mags[3], (uint64_t)c->cur};
+    hipGraphExec_t exec = nullptr;
+    for (auto& g : c->graphs)
+      if (g.key == key) exec = g.exec;
+    if (!exec) {
+      if (c->graphs.size() >= 16) {
+        for (auto& g : c->graphs) {
+          (void)hipGraphExecDestroy(g.exec);
+          (void)hipGraphDestroy(g.graph);
+        }
+        c->graphs.clear();
+      }
+      const int cur0 = c->cur;
+      HIPC(c, hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
+      e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->cap);
+      hipGraph_t graph = nullptr;
+      const hipError_t ce = hipStreamEndCapture(c->cap, &graph);
+      if (e) return e;
+      if (ce != hipSuccess) return fail(c, OMEGA_EHIP, "graph capture: %s", hipGetErrorString(ce));
+      HIPC(c, hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      c->graphs.push_back({key, graph, exec});
+      c->cur = cur0;  // capture advanced the parity; the replay below advances it for real
+    }
+    HIPC(c, hipGraphLaunch(exec, c->stream));
+    if (meters) {
+      const int64_t chunk = std::min<int64_t>(4096, kSortCapHost - c->HL);
+      const int64_t nchunks = (n_frames + chunk - 1) / chunk;
+      c->cur ^= (int)(nchunks & 1);
+    }
+    return 0;
   }
+  e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->stream);
+  if (e) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 }
@@ -838,7 +946,7 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
     if (!e) e = stage_out(c, 4, meters, ncf * 5, outs, &dm);
     if (e) return e;
   }
-  e = meters_enqueue(c, dl, dt, n_frames, dm);
+  e = meters_enqueue(c, dl, dt, n_frames, dm, c->stream);
   if (e) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;

@@ -112,89 +112,127 @@ __device__ __forceinline__ int swz(int i) {
   }
 }
 
-// One Stockham pass over K points with NTH threads: butterfly j in [0, K/R) reads j + r*K/R
-// (r < R), multiplies by w^(r*k) with k = j mod NS and w = exp(-2 pi i / (NS*R)), DFTs, and writes
-// output m to (j/NS)*NS*R + k + m*NS. PNS/PR name the previous pass (its swizzle is our read
-// swizzle).
-template <int K, int R, int NS, int PNS, int PR, int NTH>
-__device__ __forceinline__ void stockham_pass(float2* buf, const float2* __restrict__ tw, int tid) {
+// One Stockham pass over K points with NTH threads: butterfly j in [0, K/R) reads logical elements
+// j + r*K/R (r < R) through `load`, multiplies element r by w^(r*k) with k = j mod NS and
+// w = exp(-2 pi i / (NS*R)), DFTs, and hands output m to `store` at logical index
+// (j/NS)*NS*R + k + m*NS. The twiddle base is fetched before the loads (its global-memory latency
+// overlaps the LDS reads and the barrier) and its powers are formed by a multiply chain (two live
+// registers instead of R). SYNC_MID: loads and stores hit the same LDS buffer in place, so a
+// barrier separates all reads from all writes.
+template <int K, int R, int NS, int NTH, bool SYNC_MID, class Load, class Store>
+__device__ __forceinline__ void fft_pass(const float2* __restrict__ tw, int tid, Load&& load, Store&& store) {
   constexpr int NB = K / R;
   constexpr int B = (NB + NTH - 1) / NTH;
   float2 v[B][R];
+  float2 w1[B];
   static_for<0, B>([&](auto b) {
     const int j = tid + b * NTH;
-    if (NB % NTH == 0 || j < NB) {
-      static_for<0, R>([&](auto r) { v[b][r] = buf[swz<PNS, PR>(j + r * NB)]; });
+    if constexpr (NS > 1) {
+      if (NB % NTH == 0 || j < NB) w1[b] = tw[(j & (NS - 1)) * (K / (NS * R))];
     }
   });
-  __syncthreads();
+  static_for<0, B>([&](auto b) {
+    const int j = tid + b * NTH;
+    if (NB % NTH == 0 || j < NB) static_for<0, R>([&](auto r) { v[b][r] = load(j + r * NB); });
+  });
+  if constexpr (SYNC_MID) __syncthreads();
   static_for<0, B>([&](auto b) {
     const int j = tid + b * NTH;
     if (NB % NTH == 0 || j < NB) {
       const int k = j & (NS - 1);
       if constexpr (NS > 1) {
-        // twiddle w^r, w = exp(-2 pi i k / (NS R)) = tw[k * K / (NS R)]
-        const float2 w1 = tw[k * (K / (NS * R))];
-        float2 wp[R];
-        wp[1] = w1;
-        static_for<2, R>([&](auto r) {
-          constexpr int hi = 1 << ilog2(r);  // highest power of two <= r
-          if constexpr (hi == r)
-            wp[r] = cmul(wp[r / 2], wp[r / 2]);
-          else
-            wp[r] = cmul(wp[hi], wp[r - hi]);
+        float2 w = w1[b];
+        static_for<1, R>([&](auto r) {
+          v[b][r] = cmul(v[b][r], w);
+          if constexpr (r + 1 < R) w = cmul(w, w1[b]);
         });
-        static_for<1, R>([&](auto r) { v[b][r] = cmul(v[b][r], wp[r]); });
       }
       dft_dif<R>(v[b]);
       const int base = (j / NS) * NS * R + k;
-      static_for<0, R>([&](auto m) { buf[swz<NS, R>(base + m * NS)] = v[b][brev<R>(m)]; });
+      static_for<0, R>([&](auto m) { store(base + m * NS, v[b][brev<R>(m)]); });
     }
   });
-  __syncthreads();
 }
 
-// A radix plan R0, R1, ... applied in order with NS = product of the radices before each pass.
+// Radix plan R0, R1, ... applied in order with NS = product of the radices before each pass.
+// FIRST/LAST: whether the first pass loads through `first` (e.g. straight from global memory) and
+// the last pass stores through `last` (e.g. a register-side reduction) instead of the LDS buffer.
 template <int K, int NTH, int NS, int PNS, int PR, int... Rs>
 struct StockhamChain;
 template <int K, int NTH, int NS, int PNS, int PR>
 struct StockhamChain<K, NTH, NS, PNS, PR> {
-  static __device__ __forceinline__ void run(float2*, const float2*, int) {}
+  template <bool FIRST, bool LAST, class F, class G>
+  static __device__ __forceinline__ void run(float2*, const float2*, int, F&&, G&&) {}
   static __device__ __forceinline__ int out(int i) { return swz<PNS, PR>(i); }
 };
 template <int K, int NTH, int NS, int PNS, int PR, int R, int... Rs>
 struct StockhamChain<K, NTH, NS, PNS, PR, R, Rs...> {
-  static __device__ __forceinline__ void run(float2* b, const float2* tw, int t) {
-    stockham_pass<K, R, NS, PNS, PR, NTH>(b, tw, t);
-    StockhamChain<K, NTH, NS * R, NS, R, Rs...>::run(b, tw, t);
+  using Next = StockhamChain<K, NTH, NS * R, NS, R, Rs...>;
+  static constexpr bool kLastPass = sizeof...(Rs) == 0;
+  template <bool FIRST, bool LAST, class F, class G>
+  static __device__ __forceinline__ void run(float2* buf, const float2* tw, int t, F&& first, G&& last) {
+    auto lds_load = [&](int i) { return buf[swz<PNS, PR>(i)]; };
+    auto lds_store = [&](int i, float2 v) { buf[swz<NS, R>(i)] = v; };
+    constexpr bool in_global = FIRST && NS == 1;
+    constexpr bool out_regs = LAST && kLastPass;
+    // in place in LDS needs the mid-pass barrier; a global-source or register-sink pass does not
+    constexpr bool sync_mid = !in_global && !out_regs;
+    if constexpr (in_global && out_regs)
+      fft_pass<K, R, NS, NTH, false>(tw, t, first, last);
+    else if constexpr (in_global)
+      fft_pass<K, R, NS, NTH, false>(tw, t, first, lds_store);
+    else if constexpr (out_regs)
+      fft_pass<K, R, NS, NTH, false>(tw, t, lds_load, last);
+    else
+      fft_pass<K, R, NS, NTH, sync_mid>(tw, t, lds_load, lds_store);
+    if constexpr (!out_regs) __syncthreads();  // results visible to the next pass / the caller
+    Next::template run<FIRST, LAST>(buf, tw, t, first, last);
   }
-  static __device__ __forceinline__ int out(int i) { return StockhamChain<K, NTH, NS * R, NS, R, Rs...>::out(i); }
+  static __device__ __forceinline__ int out(int i) { return Next::out(i); }
 };
 
-// Forward complex FFT of K points in LDS with NTH threads (natural order in, identity swizzle;
-// natural order out at index out(i)). tw: exp(-2 pi i m / K), m < K. The caller has synchronised
-// after filling buf; run() ends with a barrier.
+// Forward complex FFT of K points with NTH threads. Natural order in (identity swizzle) and out
+// (element i at buf[out(i)]). tw: exp(-2 pi i m / K), m < K. run(): input already in LDS and the
+// caller synchronised; run_from(first): the first pass reads logical element i as first(i) (no LDS
+// write of the input; the caller must make sure no one still reads buf); run_to(last): the last pass
+// hands outputs to last(i, v) instead of LDS (the caller synchronises before reusing buf).
+template <int K, int NTH, int... Rs>
+struct FFTPlan {
+  using Chain = StockhamChain<K, NTH, 1, 0, 1, Rs...>;
+  static __device__ __forceinline__ void run(float2* b, const float2* tw, int t) {
+    auto none = [](int) { return make_float2(0.f, 0.f); };
+    auto sink = [](int, float2) {};
+    Chain::template run<false, false>(b, tw, t, none, sink);
+  }
+  template <class F>
+  static __device__ __forceinline__ void run_from(float2* b, const float2* tw, int t, F&& first) {
+    auto sink = [](int, float2) {};
+    Chain::template run<true, false>(b, tw, t, first, sink);
+  }
+  template <class G>
+  static __device__ __forceinline__ void run_to(float2* b, const float2* tw, int t, G&& last) {
+    auto none = [](int) { return make_float2(0.f, 0.f); };
+    Chain::template run<false, true>(b, tw, t, none, last);
+  }
+  static __device__ __forceinline__ int out(int i) { return Chain::out(i); }
+};
+
+// Plans: a small twiddle-free first radix, then radix-16 passes; NTH = K/16 threads so every
+// radix-16 pass is one butterfly per thread.
+template <int K>
+constexpr int threads_for() { return K / 16 < 64 ? 64 : (K / 16 > 512 ? 512 : K / 16); }
+
 template <int K, int NTH>
 struct BlockFFTPlan;
-template <int NTH> struct BlockFFTPlan<8192, NTH> {
-  // 512 threads: four passes of at most 16 values per thread (fits the 128-VGPR budget of two
-  // 8-wave workgroups per CU); 256 threads: three passes
-  using type = typename std::conditional<NTH >= 512, StockhamChain<8192, NTH, 1, 0, 1, 16, 16, 16, 2>,
-                                         StockhamChain<8192, NTH, 1, 0, 1, 32, 16, 16>>::type;
-};
-template <int NTH> struct BlockFFTPlan<4096, NTH> { using type = StockhamChain<4096, NTH, 1, 0, 1, 16, 16, 16>; };
-template <int NTH> struct BlockFFTPlan<2048, NTH> { using type = StockhamChain<2048, NTH, 1, 0, 1, 8, 16, 16>; };
-template <int NTH> struct BlockFFTPlan<1024, NTH> { using type = StockhamChain<1024, NTH, 1, 0, 1, 4, 16, 16>; };
-template <int NTH> struct BlockFFTPlan<512, NTH> { using type = StockhamChain<512, NTH, 1, 0, 1, 2, 16, 16>; };
-template <int NTH> struct BlockFFTPlan<256, NTH> { using type = StockhamChain<256, NTH, 1, 0, 1, 16, 16>; };
+template <int NTH> struct BlockFFTPlan<8192, NTH> { using type = FFTPlan<8192, NTH, 2, 16, 16, 16>; };
+template <int NTH> struct BlockFFTPlan<4096, NTH> { using type = FFTPlan<4096, NTH, 16, 16, 16>; };
+template <int NTH> struct BlockFFTPlan<2048, NTH> { using type = FFTPlan<2048, NTH, 8, 16, 16>; };
+template <int NTH> struct BlockFFTPlan<1024, NTH> { using type = FFTPlan<1024, NTH, 4, 16, 16>; };
+template <int NTH> struct BlockFFTPlan<512, NTH> { using type = FFTPlan<512, NTH, 2, 16, 16>; };
+template <int NTH> struct BlockFFTPlan<256, NTH> { using type = FFTPlan<256, NTH, 16, 16>; };
 
-template <int K, int NTH = NT>
+template <int K, int NTH = threads_for<K>()>
 using BlockFFT = typename BlockFFTPlan<K, NTH>::type;
-
-// Threads per workgroup for a K-point transform: 8 waves for the 8192-point transforms (register
-// budget of the true-peak kernel, more waves to cover LDS latency), 4 waves otherwise.
-template <int K>
-constexpr int threads_for() { return K >= 8192 ? 512 : 256; }
 
 // ---- block reductions ----
 __device__ __forceinline__ float wave_max(float v) {

@@ -1,20 +1,22 @@
 // Meter aggregates (A9): professional_meters.py:248-279 with the deques of :20-25.
 //
 // For channel c and batch frame f the reference state after f+1 calculate_lufs calls is a window over
-// the virtual sequence V = history ++ batch[0..f]:
+// the virtual sequence V = history ++ batch[0..f] (union index u = time order):
 //   momentary  = mean(last 24 LUFS_inst)          short_term = mean(last 180)
 //   integrated = mean(g), g = {v in last 3600 : v > -70}, else -100
 //   range      = percentile(g, 95) - percentile(g, 10) (numpy 'linear'), else 0
 //   true_peak  = max(last 60 TP)
-// One wave per (frame, channel): the gated window (<= 57 values per lane) sits in registers as
-// order-preserving integer keys; each percentile is an exact radix select (32 ballot-count passes
-// over the window) plus one min-reduction for the upper neighbour.
+// Consecutive frames' windows share all but one value, so the gated union of a batch is sorted once
+// per channel (meter_sort_kernel: 64-bit keys = order-preserving value key << 32 | union index,
+// bitonic sort in LDS) and each frame's order statistics become rank queries over that sorted list
+// restricted to the frame's index range (meter_query_kernel: one wave per frame, wave-wide ballots
+// over LDS-staged keys, no per-frame sort). Batches longer than kMaxBatch frames are split by the host.
 #include "fft.hpp"
 #include "params.hpp"
 
 namespace omega {
 
-constexpr int kSlots = 57;  // ceil(3600 / 64): integrated_len <= kSlots * 64
+constexpr int kSortCap = 8192;  // union capacity: (integrated_len - 1) + batch chunk
 
 __device__ __forceinline__ uint32_t fkey(float v) {
   const uint32_t u = __float_as_uint(v);
@@ -24,101 +26,161 @@ __device__ __forceinline__ float unkey(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
-__device__ __forceinline__ float seq_at(const MeterParams& p, const float* hist, const float* batch, int nh,
-                                        int HC, int c, int64_t i) {
-  return i < nh ? hist[(int64_t)c * HC + i] : batch[(i - nh) * p.C + c];
+__device__ __forceinline__ float seq_at(const float* hist, const float* batch, int nh, int HC, int C, int c,
+                                        int64_t i) {
+  return i < nh ? hist[(int64_t)c * HC + i] : batch[(i - nh) * C + c];
 }
 
-// k-th smallest (0-based) of the gated keys
-__device__ __forceinline__ uint32_t select_rank(const uint32_t (&key)[kSlots], int nslots, int k) {
-  uint32_t prefix = 0;
-  for (int bit = 31; bit >= 0; --bit) {
-    const uint32_t cand = prefix | (1u << bit);
-    int cnt = 0;
-    static_for<0, kSlots>([&](auto s) {
-      if (s < nslots) cnt += __popcll(__ballot(key[s] < cand));
-    });
-    if (cnt <= k) prefix = cand;
-  }
-  return prefix;
-}
-
-// numpy.percentile(g, q) with method='linear' over the gated keys (n = gated count > 0)
-__device__ __forceinline__ double percentile(const uint32_t (&key)[kSlots], int nslots, int n, double q) {
-  const double vi = (double)(n - 1) * q;
-  int prev = (int)floor(vi);
-  if (vi >= (double)(n - 1)) prev = n - 1;
-  const double gamma = vi - floor(vi);
-  const uint32_t klo = select_rank(key, nslots, prev);
-  if (prev >= n - 1) return (double)unkey(klo);
-  // upper neighbour: the same value if it repeats, else the smallest key above it
-  int le = 0;
-  uint32_t above = 0xFFFFFFFFu;
-  static_for<0, kSlots>([&](auto s) {
-    if (s < nslots) {
-      le += __popcll(__ballot(key[s] <= klo));
-      if (key[s] > klo && key[s] < above) above = key[s];
+// Sort the gated union of channel c (window-relevant part only: the first frame's window start on).
+__global__ __launch_bounds__(1024) void meter_sort_kernel(MeterParams p, unsigned long long* sorted, int* n_sorted) {
+  __shared__ unsigned long long key[kSortCap];
+  __shared__ int cnt;
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int nl = p.n_hist_l[c];
+  const int64_t n = nl + p.n_frames;                    // union length
+  const int64_t u0 = max<int64_t>(0, nl + 1 - p.int_len); // first index any frame's window reaches
+  const int64_t m = n - u0;                             // <= kSortCap (host guarantees)
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  // compact the gated values (order irrelevant: the sort restores it)
+  for (int64_t i = tid; i < m; i += 1024) {
+    const float v = seq_at(p.hist_l, p.lufs, nl, p.HL, p.C, c, u0 + i);
+    if (v > p.gate) {
+      const int slot = atomicAdd(&cnt, 1);
+      key[slot] = ((unsigned long long)fkey(v) << 32) | (unsigned long long)(u0 + i);
     }
-  });
-  for (int o = 32; o >= 1; o >>= 1) above = min(above, (uint32_t)__shfl_xor((int)above, o, 64));
-  const uint32_t khi = le > prev + 1 ? klo : above;
-  const double a = unkey(klo), b = unkey(khi);
+  }
+  __syncthreads();
+  const int g = cnt;
+  int np2 = 1;
+  while (np2 < g) np2 <<= 1;
+  for (int i = g + tid; i < np2; i += 1024) key[i] = ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < np2; i += 1024) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = key[i], b = key[l];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            key[i] = b;
+            key[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  unsigned long long* out = sorted + (int64_t)c * kSortCap;
+  for (int i = tid; i < g; i += 1024) out[i] = key[i];
+  if (tid == 0) n_sorted[c] = g;
+}
+
+// numpy 'linear' percentile from the two neighbouring order statistics
+__device__ __forceinline__ double lerp_pct(double a, double b, double gamma) {
   const double d = b - a;  // numpy _lerp
   return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
 }
 
-__global__ __launch_bounds__(256) void meter_agg_kernel(MeterParams p) {
-  const int lane = threadIdx.x & 63;
-  const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // output index f*C + c
-  if (o >= p.n_frames * p.C) return;
-  const int64_t f = o / p.C;
-  const int c = (int)(o % p.C);
+// One wave per output (f, c); a 256-thread block serves 4 consecutive frames of one channel and
+// stages the channel's sorted union in LDS once.
+__global__ __launch_bounds__(256) void meter_query_kernel(MeterParams p, const unsigned long long* sorted,
+                                                          const int* n_sorted) {
+  __shared__ unsigned long long key[kSortCap];
+  const int c = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = n_sorted[c];
+  const unsigned long long* src = sorted + (int64_t)c * kSortCap;
+  for (int i = tid; i < g; i += 256) key[i] = src[i];
+  __syncthreads();
+  const int64_t f = (int64_t)blockIdx.x * 4 + (tid >> 6);
+  if (f >= p.n_frames) return;
   const int nl = p.n_hist_l[c], nt = p.n_hist_t[c];
-  const int64_t n = nl + f + 1;  // length of the LUFS sequence
-  // momentary / short-term: dB-domain means of the last 24 / 180 values
+  const int64_t n = nl + f + 1;  // sequence length after this frame
+  // momentary / short-term: dB-domain means of the last 24 / 180 values (ungated, time order)
   double sm = 0.0, ss = 0.0;
   const int64_t wm = min<int64_t>(p.mom_len, n), ws = min<int64_t>(p.short_len, n);
   for (int64_t i = lane; i < ws; i += 64) {
-    const double v = seq_at(p, p.hist_l, p.lufs, nl, p.HL, c, n - ws + i);
+    const double v = seq_at(p.hist_l, p.lufs, nl, p.HL, p.C, c, n - ws + i);
     ss += v;
     if (i >= ws - wm) sm += v;
   }
   sm = wave_sum(sm);
   ss = wave_sum(ss);
-  // integrated window: gated keys in registers
+  // integrated window [lo, hi] in union indices; members of the sorted gated list with index in range
   const int64_t wi = min<int64_t>(p.int_len, n);
-  const int nslots = (int)((wi + 63) / 64);
-  uint32_t key[kSlots];
+  const uint32_t lo = (uint32_t)(n - wi), hi = (uint32_t)(n - 1);
+  const int rows = (g + 63) / 64;
+  int ng = 0;
   double gs = 0.0;
-  int gc = 0;
-  static_for<0, kSlots>([&](auto s) {
-    key[s] = 0xFFFFFFFFu;
-    if (s < nslots) {
-      const int64_t i = (int64_t)s * 64 + lane;
-      if (i < wi) {
-        const float v = seq_at(p, p.hist_l, p.lufs, nl, p.HL, c, n - wi + i);
-        if (v > p.gate) {
-          key[s] = fkey(v);
-          gs += v;
-          gc += 1;
+  for (int r = 0; r < rows; ++r) {
+    const int i = r * 64 + lane;
+    bool mem = false;
+    if (i < g) {
+      const uint32_t t = (uint32_t)key[i];
+      mem = t >= lo && t <= hi;
+      if (mem) gs += unkey((uint32_t)(key[i] >> 32));
+    }
+    ng += __popcll(__ballot(mem));
+  }
+  gs = wave_sum(gs);
+  double integ = -100.0, range = 0.0;
+  if (ng > 0) {
+    integ = gs / ng;
+    // ranks needed: floor((n-1) q) and the next one, for q = 0.10 and 0.95
+    int want[4];
+    double gam[2];
+    const double qs[2] = {0.10, 0.95};
+    for (int q = 0; q < 2; ++q) {
+      const double vi = (double)(ng - 1) * qs[q];
+      int prev = (int)floor(vi);
+      if (vi >= (double)(ng - 1)) prev = ng - 1;
+      want[2 * q] = prev;
+      want[2 * q + 1] = min(prev + 1, ng - 1);
+      gam[q] = vi - floor(vi);
+    }
+    float val[4];
+    // second sweep: running member count per row finds the requested ranks
+    int base = 0;
+    int found = 0;
+    for (int r = 0; r < rows && found < 4; ++r) {
+      const int i = r * 64 + lane;
+      bool mem = false;
+      uint32_t kv = 0;
+      if (i < g) {
+        const uint32_t t = (uint32_t)key[i];
+        mem = t >= lo && t <= hi;
+        kv = (uint32_t)(key[i] >> 32);
+      }
+      const unsigned long long b = __ballot(mem);
+      const int rc = __popcll(b);
+      const int before = __popcll(b & ((1ull << lane) - 1ull));  // members in lanes below
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int k = want[w];
+        if (k >= base && k < base + rc) {
+          // the lane holding member rank k of this row broadcasts its value
+          const unsigned long long hit = __ballot(mem && before == k - base);
+          const int src_lane = __ffsll((long long)hit) - 1;
+          val[w] = unkey((uint32_t)__shfl((int)kv, src_lane, 64));
         }
       }
+      base += rc;
+      found = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) found += want[w] < base;
     }
-  });
-  gs = wave_sum(gs);
-  for (int off = 32; off >= 1; off >>= 1) gc += __shfl_xor(gc, off, 64);
-  double integ = -100.0, range = 0.0;
-  if (gc > 0) {
-    integ = gs / gc;
-    range = percentile(key, nslots, gc, 0.95) - percentile(key, nslots, gc, 0.10);
+    // at the top end numpy takes the last element twice: b - a = 0 and either _lerp branch gives it
+    range = lerp_pct(val[2], val[3], gam[1]) - lerp_pct(val[0], val[1], gam[0]);
   }
   // true-peak hold
   const int64_t ntp = nt + f + 1, wt = min<int64_t>(p.peak_len, ntp);
   float tpm = -INFINITY;
-  for (int64_t i = lane; i < wt; i += 64) tpm = fmaxf(tpm, seq_at(p, p.hist_t, p.tp, nt, p.HT, c, ntp - wt + i));
+  for (int64_t i = lane; i < wt; i += 64) tpm = fmaxf(tpm, seq_at(p.hist_t, p.tp, nt, p.HT, p.C, c, ntp - wt + i));
   tpm = wave_max(tpm);
   if (lane == 0) {
-    double* out = p.out + o * 5;
+    double* out = p.out + (f * p.C + c) * 5;
     out[0] = sm / (double)wm;
     out[1] = ss / (double)ws;
     out[2] = integ;
@@ -147,10 +209,14 @@ __global__ __launch_bounds__(256) void meter_state_kernel(MeterStateParams p) {
   }
 }
 
-hipError_t launch_meters(const MeterParams& p, const MeterStateParams& sp, hipStream_t s) {
-  const int64_t nout = p.n_frames * p.C;
-  hipLaunchKernelGGL(meter_agg_kernel, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, s, p);
+hipError_t launch_meters(const MeterParams& p, const MeterStateParams& sp, unsigned long long* sorted, int* n_sorted,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(meter_sort_kernel, dim3((unsigned)p.C), dim3(1024), 0, s, p, sorted, n_sorted);
   hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(meter_query_kernel, dim3((unsigned)((p.n_frames + 3) / 4), (unsigned)p.C), dim3(256), 0, s, p,
+                     sorted, n_sorted);
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(meter_state_kernel, dim3((unsigned)p.C), dim3(256), 0, s, sp);
   return hipGetLastError();

@@ -78,12 +78,11 @@ __global__ __launch_bounds__(NTH, 2 * NTH / 256) void mrfft_kernel(SpectralParam
   const float* __restrict__ x = p.x + f * p.frame_stride + c * p.chan_stride + rp.offset;
   const float2* x2 = reinterpret_cast<const float2*>(x);
   const float2* w2 = reinterpret_cast<const float2*>(rp.win);
-  for (int n = tid; n < K; n += NTH) {
-    const float2 a = x2[n], w = w2[n];
-    buf[n] = make_float2(a.x * w.x, a.y * w.y);
-  }
-  __syncthreads();
-  BlockFFT<K, NTH>::run(buf, p.tw[ilog2(K)], tid);
+  // the first FFT pass reads the windowed frame straight from global memory (coalesced float2)
+  BlockFFT<K, NTH>::run_from(buf, p.tw[ilog2(K)], tid, [&](int i) {
+    const float2 a = x2[i], w = w2[i];
+    return make_float2(a.x * w.x, a.y * w.y);
+  });
   rfft_magnitudes<K, NTH>(buf, p.tw[ilog2(2 * K)], tid);
   const float* mag = reinterpret_cast<const float*>(buf);
   const float* __restrict__ wgt = rp.wgt;
@@ -117,9 +116,8 @@ __global__ __launch_bounds__(NTH, 2 * NTH / 256) void mrfft_kernel(SpectralParam
 }
 
 // True peak of one frame of M = 2K samples (dBTP; float32 like scipy on float32 input).
-// (K = 8192 with 512 threads needs ~160 VGPRs: one 8-wave workgroup per CU, launch bound 2 waves/SIMD)
 template <int K, int NTH = threads_for<K>()>
-__global__ __launch_bounds__(NTH, K >= 8192 ? 2 : 2 * NTH / 256) void truepeak_kernel(SpectralParams p) {
+__global__ __launch_bounds__(NTH, 2) void truepeak_kernel(SpectralParams p) {
   constexpr int M = 2 * K;
   using FFT = BlockFFT<K, NTH>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -129,14 +127,12 @@ __global__ __launch_bounds__(NTH, K >= 8192 ? 2 : 2 * NTH / 256) void truepeak_k
   const int64_t cf = blockIdx.x;
   const int64_t f = cf / p.C, c = cf % p.C;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride);
-  float mx = 0.f;
-  for (int n = tid; n < K; n += NTH) {
-    const float2 a = x2[n];
-    buf[n] = a;
+  float mx = 0.f;  // p = 0 phase: the samples themselves (every one is loaded exactly once below)
+  FFT::run_from(buf, p.tw[ilog2(K)], tid, [&](int i) {
+    const float2 a = x2[i];
     mx = fmaxf(mx, fmaxf(fabsf(a.x), fabsf(a.y)));
-  }
-  __syncthreads();
-  FFT::run(buf, p.tw[ilog2(K)], tid);
+    return a;
+  });
   const float2* __restrict__ twM = p.tw[ilog2(M)];
   constexpr int NP = K / 2;  // pairs (k, K-k), k < K/2; k = 0 carries X[0], X[K] and X[K/2]
   constexpr int PB = (NP + NTH - 1) / NTH;
@@ -198,11 +194,8 @@ __global__ __launch_bounds__(NTH, K >= 8192 ? 2 : 2 * NTH / 256) void truepeak_k
       }
     });
     __syncthreads();
-    FFT::run(buf, twK, tl);
-    for (int n = tl; n < K; n += NTH) {
-      const float2 z = buf[n];
-      fmx = fmaxf(fmx, fmaxf(fabsf(z.x), fabsf(z.y)));
-    }
+    // the last pass reduces straight from registers: no LDS write of the inverse transform
+    FFT::run_to(buf, twK, tl, [&](int, float2 z) { fmx = fmaxf(fmx, fmaxf(fabsf(z.x), fabsf(z.y))); });
   }
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
   if (tid == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
@@ -218,12 +211,10 @@ __global__ __launch_bounds__(NTH, 2 * NTH / 256) void rfft_kernel(RfftParams p) 
   const int64_t i = blockIdx.x;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + i * (2 * K));
   const float2* w2 = reinterpret_cast<const float2*>(p.win);
-  for (int n = tid; n < K; n += NTH) {
+  FFT::run_from(buf, p.tw[ilog2(K)], tid, [&](int n) {
     const float2 a = x2[n], w = w2[n];
-    buf[n] = make_float2(a.x * w.x, a.y * w.y);
-  }
-  __syncthreads();
-  FFT::run(buf, p.tw[ilog2(K)], tid);
+    return make_float2(a.x * w.x, a.y * w.y);
+  });
   const float2* __restrict__ twN = p.tw[ilog2(2 * K)];
   float2* cp = p.cplx ? reinterpret_cast<float2*>(p.cplx) + i * (K + 1) : nullptr;
   float* mp = p.mag ? p.mag + i * (K + 1) : nullptr;
@@ -283,8 +274,8 @@ __global__ __launch_bounds__(256) void combine_kernel(CombineParams p) {
     default: return hipErrorInvalidValue; \
   }
 
-// Resolution kernels (in resolution order), then the true-peak kernel for frames of W samples.
-hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s) {
+// Resolution kernels, in resolution order (the combine owner protocol relies on it).
+hipError_t launch_mrfft(const SpectralParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
   for (int r = 0; r < p.n_res; ++r) {
     if (!p.comb_out && !p.res[r].mag_out) continue;
@@ -295,6 +286,12 @@ hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
+  return hipSuccess;
+}
+
+// The true-peak kernel for frames of W samples.
+hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)p.n_cf);
   if (p.tp_out) {
 #define OMEGA_TP(K) \
   hipLaunchKernelGGL(truepeak_kernel<K>, grid, dim3(threads_for<K>()), K * sizeof(float2) + 16 * sizeof(float), \
@@ -303,6 +300,11 @@ hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s) {
 #undef OMEGA_TP
   }
   return hipGetLastError();
+}
+
+hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s) {
+  const hipError_t e = launch_mrfft(p, s);
+  return e != hipSuccess ? e : launch_truepeak(W, p, s);
 }
 
 hipError_t launch_combine(const CombineParams& p, hipStream_t s) {

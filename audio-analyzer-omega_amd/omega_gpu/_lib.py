@@ -54,6 +54,7 @@ EXPORTS = {
     "omega_last_error": (C.c_char_p, [C.c_void_p]),
     "omega_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "omega_synchronize": (C.c_int, [C.c_void_p]),
+    "omega_set_graphs": (C.c_int, [C.c_void_p, C.c_int]),
     "omega_process_frames": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64,
                                        C.POINTER(Outputs), C.c_int]),
     "omega_combine": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int64, C.c_void_p, C.c_int]),
@@ -77,10 +78,31 @@ EXPORTS = {
 _lib = None
 
 
+def _share_torch_hip_runtime() -> None:
+    """One HIP runtime per process. torch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7,
+    like /opt/rocm's). If libomega loaded first it would bind /opt/rocm's copy and torch would then
+    load a second runtime (torch reports "No HIP GPUs are available", and torch streams/events would
+    not order libomega's kernels). Preloading torch's copy by path, without importing torch, makes
+    libomega's NEEDED libamdhip64.so.7 resolve to the runtime torch uses."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
+            return
+
+
 def lib() -> C.CDLL:
     """Load libomega.so once (raises if the HIP library was not built: no fallback)."""
     global _lib
     if _lib is None:
+        _share_torch_hip_runtime()
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libomega.so not found at {LIB_PATH}; run `make -C audio-analyzer-omega_amd` "
                               "(or __graft_entry__.build())")

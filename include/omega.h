@@ -107,8 +107,13 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out);
 void omega_destroy(omega_ctx* ctx);
 const char* omega_last_error(const omega_ctx* ctx);
 const char* omega_version(void);
-/* Use a caller-owned hipStream_t (NULL restores the context's own stream). */
+/* Enqueue on a caller-owned hipStream_t (NULL = the null/default stream, e.g. PyTorch's default
+ * stream). Contexts start on a private non-blocking stream. */
 int omega_set_stream(omega_ctx* ctx, void* hip_stream);
+/* Device-memory omega_process_frames calls are captured once per distinct argument set into a HIP
+ * graph (three concurrent branches: resolution kernels / true peak / K-weighting, joined before the
+ * meter aggregates) and replayed afterwards. Enabled by default; 0 launches directly. */
+int omega_set_graphs(omega_ctx* ctx, int enable);
 int omega_synchronize(omega_ctx* ctx);
 
 /* The fused per-channel-frame hot path over n_frames x n_channels frames of W samples. */

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Run one stage of the cfg2 hot path in isolation (for rocprofv3 counter passes and A/B timing).
+
+  python tools/kernel_bench.py {tp,kw,mrfft,meters,all} [--reps N]
+"""
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "audio-analyzer-omega_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("stage")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import bench
+    from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
+    from omega_gpu import _lib as L
+    x = torch.from_numpy(bench.cfg2_input()).cuda()
+    eng = Engine(NORTHSTAR_RESOLUTIONS, 48000, 20000, target_bins=512, n_channels=2)
+    ncf = 512
+    lib = L.lib()
+    eng._bind_stream(x)
+    out = {k: torch.empty(ncf, device="cuda") for k in ("tp", "li")}
+    comb = torch.empty(ncf, 512, device="cuda")
+    met = torch.empty(ncf, 5, dtype=torch.float64, device="cuda")
+
+    def run():
+        if a.stage in ("tp", "all"):
+            eng._check(lib.omega_true_peak(eng._ctx, x.data_ptr(), ncf, 16384, out["tp"].data_ptr(), L.MEM_DEVICE))
+        if a.stage in ("kw", "all"):
+            eng._check(lib.omega_k_weighting(eng._ctx, x.data_ptr(), ncf, 16384, None, out["li"].data_ptr(), L.MEM_DEVICE))
+        if a.stage in ("mrfft", "all"):
+            eng.process_frames(x, 256, 2 * 16384, 16384, combined=True, lufs=False, true_peak=False,
+                               out={"combined": comb})
+        if a.stage in ("meters", "all"):
+            eng._check(lib.omega_meter_update(eng._ctx, out["li"].data_ptr(), out["tp"].data_ptr(), 256,
+                                              met.data_ptr(), L.MEM_DEVICE))
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(a.reps):
+        run()
+    e.record()
+    torch.cuda.synchronize()
+    print(f"{a.stage}: {s.elapsed_time(e) / a.reps * 1e3:.1f} us per call")
+
+
+if __name__ == "__main__":
+    main()
