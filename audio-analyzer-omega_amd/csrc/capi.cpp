@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -23,11 +24,11 @@
 namespace omega {
 hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_mrfft(const SpectralParams& p, hipStream_t s);
+hipError_t launch_mrfft_range(const SpectralParams& p, int r0, int r1, hipStream_t s);
 hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
-hipError_t launch_meters(const MeterParams& p, const MeterStateParams& sp, unsigned long long* sorted, int* n_sorted,
-                         hipStream_t s);
+hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_bands(const BandParams& p, hipStream_t s);
 hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int hi, const double* mat, double* out,
                          hipStream_t s);
@@ -39,7 +40,8 @@ using namespace omega;
 namespace {
 
 constexpr double kPi = 3.14159265358979323846;
-constexpr int kSortCapHost = 8192;  // meters.hip kSortCap
+constexpr int kUnionCapHost = 8192;  // meters.hip kUnionCap (4096 history + 4096 batch)
+constexpr int kChunkFrames = 4096;   // meters.hip kNewCap
 
 struct DevBuf {
   void* p = nullptr;
@@ -149,6 +151,10 @@ struct omega_ctx {
   hipStream_t cap = nullptr, fork[2] = {nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   bool use_graph = true;
+  bool concurrent = true;   // overlap the latency-bound stages (small FFTs, meters) with full-chip ones
+  bool res_independent = false;  // no combine target has several owners: resolution kernels commute
+  int layout = 2;                // concurrent layouts (OMEGA_LAYOUT for A/B runs): 1 meters only, 2 full
+  hipEvent_t ev_kw = nullptr;
   struct GraphEntry {
     std::vector<uint64_t> key;
     hipGraph_t graph;
@@ -181,8 +187,13 @@ struct omega_ctx {
   int* d_nl[2] = {};
   int* d_nt[2] = {};
   int cur = 0;
-  unsigned long long* d_sorted = nullptr;  // [C, 8192] gated union keys (meter_sort_kernel scratch)
-  int* d_nsorted = nullptr;
+  unsigned long long* d_skeys[2] = {};  // sorted gated history keys (double-buffered state)
+  int* d_ns[2] = {};
+  uint32_t* d_t0[2] = {};
+  unsigned long long* d_union = nullptr;  // per-batch scratch
+  int* d_nunion = nullptr;
+  int* d_gcount = nullptr;
+  double* d_gsum = nullptr;
   int HL = 0, HT = 0;
   // staging for OMEGA_MEM_HOST
   std::vector<DevBuf> stage;
@@ -409,6 +420,9 @@ int build_spectral_tables(omega_ctx* c) {
       own[t].push_back(en);
     }
   }
+  c->res_independent = true;
+  for (int t = 0; t < T; ++t)
+    if (own[t].size() > 1) c->res_independent = false;
   std::vector<std::vector<int>> et(cfg.n_res), ej(cfg.n_res);
   std::vector<std::vector<float>> ef(cfg.n_res);
   std::vector<float> wsum(T, 0.f);
@@ -471,8 +485,16 @@ int build_meter_state(omega_ctx* c) {
     if (!e) e = dalloc(c, &c->d_nt[b], C);
     if (e) return e;
   }
-  int e = dalloc(c, &c->d_sorted, (size_t)C * kSortCapHost);
-  if (!e) e = dalloc(c, &c->d_nsorted, C);
+  int e = 0;
+  for (int b = 0; b < 2 && !e; ++b) {
+    e = dalloc(c, &c->d_skeys[b], (size_t)C * c->HL);
+    if (!e) e = dalloc(c, &c->d_ns[b], C);
+    if (!e) e = dalloc(c, &c->d_t0[b], C);
+  }
+  if (!e) e = dalloc(c, &c->d_union, (size_t)C * kUnionCapHost);
+  if (!e) e = dalloc(c, &c->d_nunion, C);
+  if (!e) e = dalloc(c, &c->d_gcount, (size_t)C * (kUnionCapHost + 1));
+  if (!e) e = dalloc(c, &c->d_gsum, (size_t)C * (kUnionCapHost + 1));
   if (e) return e;
   return omega_meter_reset(c);
 }
@@ -539,22 +561,33 @@ int finish_host(omega_ctx* c, const std::vector<HostOut>& outs) {
   return 0;
 }
 
-// The sorted-union scratch holds (integrated_len - 1) history values plus one chunk of frames.
+// Meter aggregates over n_frames x C values, in chunks of at most kChunkFrames frames; each chunk
+// reads the state buffers `cur` and writes `cur ^ 1`.
 int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_frames, double* out,
                    hipStream_t stream) {
   const int C = c->cfg.n_channels;
-  const int64_t chunk = std::min<int64_t>(4096, kSortCapHost - c->HL);
-  for (int64_t f0 = 0; f0 < n_frames; f0 += chunk) {
-    const int64_t nf = std::min(chunk, n_frames - f0);
-    MeterParams p{};
+  for (int64_t f0 = 0; f0 < n_frames; f0 += kChunkFrames) {
+    const int64_t nf = std::min<int64_t>(kChunkFrames, n_frames - f0);
+    const int a = c->cur, b = c->cur ^ 1;
+    MeterPrepParams p{};
     p.lufs = lufs + f0 * C;
     p.tp = tp + f0 * C;
     p.n_frames = nf;
     p.C = C;
-    p.hist_l = c->d_hist_l[c->cur];
-    p.hist_t = c->d_hist_t[c->cur];
-    p.n_hist_l = c->d_nl[c->cur];
-    p.n_hist_t = c->d_nt[c->cur];
+    p.hist_l_in = c->d_hist_l[a];
+    p.hist_t_in = c->d_hist_t[a];
+    p.n_l_in = c->d_nl[a];
+    p.n_t_in = c->d_nt[a];
+    p.skeys_in = c->d_skeys[a];
+    p.n_s_in = c->d_ns[a];
+    p.t0_in = c->d_t0[a];
+    p.hist_l_out = c->d_hist_l[b];
+    p.hist_t_out = c->d_hist_t[b];
+    p.n_l_out = c->d_nl[b];
+    p.n_t_out = c->d_nt[b];
+    p.skeys_out = c->d_skeys[b];
+    p.n_s_out = c->d_ns[b];
+    p.t0_out = c->d_t0[b];
     p.HL = c->HL;
     p.HT = c->HT;
     p.mom_len = c->cfg.momentary_len;
@@ -562,51 +595,74 @@ int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_f
     p.int_len = c->cfg.integrated_len;
     p.peak_len = c->cfg.peak_len;
     p.gate = (float)c->cfg.gate_lufs;
+    p.union_keys = c->d_union;
+    p.n_union = c->d_nunion;
+    p.gcount = c->d_gcount;
+    p.gsum = c->d_gsum;
     p.out = out + f0 * C * OMEGA_N_METERS;
-    MeterStateParams s{};
-    s.lufs = p.lufs;
-    s.tp = p.tp;
-    s.n_frames = nf;
-    s.C = C;
-    s.hist_l_in = p.hist_l;
-    s.hist_t_in = p.hist_t;
-    s.n_l_in = p.n_hist_l;
-    s.n_t_in = p.n_hist_t;
-    const int nx = c->cur ^ 1;
-    s.hist_l_out = c->d_hist_l[nx];
-    s.hist_t_out = c->d_hist_t[nx];
-    s.n_l_out = c->d_nl[nx];
-    s.n_t_out = c->d_nt[nx];
-    s.HL = c->HL;
-    s.HT = c->HT;
-    HIPC(c, launch_meters(p, s, c->d_sorted, c->d_nsorted, stream));
-    c->cur = nx;
+    HIPC(c, launch_meters(p, stream));
+    c->cur = b;
   }
   return 0;
 }
 
-// The per-batch work as three branches forked from `s` and joined back on it:
-//   s:        multi-resolution kernels (resolution order)
-//   fork[0]:  true peak          fork[1]: K-weighting + LUFS
-//   s:        meter aggregates (after the join: they need LUFS and true peak)
+// The per-batch work. Sequential: resolution kernels, true peak, K-weighting, meters on `s`.
+// Concurrent (default): the full-chip kernels stay on `s` (true peak -> K-weighting -> the largest
+// resolution), the other resolution kernels run on fork[0] from the start (all of them, in order, when
+// combine targets have several owners), and the meter aggregates -- a few latency-bound workgroups --
+// run on fork[1] as soon as K-weighting is done; both branches join back into `s`.
 int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, int64_t n_frames,
                    const float* lufs, const float* tp, double* meters, hipStream_t s) {
   const bool do_tp = sp.tp_out != nullptr, do_kw = kp.lufs_out || kp.weighted_out;
+  const bool do_res = sp.comb_out != nullptr || sp.res[0].mag_out || sp.res[1].mag_out || sp.res[2].mag_out ||
+                      sp.res[3].mag_out;
+  if (!c->concurrent) {
+    if (do_res) HIPC(c, launch_mrfft(sp, s));
+    if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
+    if (do_kw) HIPC(c, launch_kweight(W, kp, s));
+    return meters ? meters_enqueue(c, lufs, tp, n_frames, meters, s) : 0;
+  }
+  int rb = 0;
+  for (int r = 1; r < sp.n_res; ++r)
+    if (sp.res[r].n > sp.res[rb].n) rb = r;
+  const bool split = c->res_independent;
+  if (c->layout == 1) {  // only the meter aggregates on a side branch
+    if (do_res) HIPC(c, launch_mrfft(sp, s));
+    if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
+    if (do_kw) HIPC(c, launch_kweight(W, kp, s));
+    if (meters) {
+      HIPC(c, hipEventRecord(c->ev_kw, s));
+      HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_kw, 0));
+      const int e = meters_enqueue(c, lufs, tp, n_frames, meters, c->fork[1]);
+      if (e) return e;
+      HIPC(c, hipEventRecord(c->ev_join[1], c->fork[1]));
+      HIPC(c, hipStreamWaitEvent(s, c->ev_join[1], 0));
+    }
+    return 0;
+  }
   HIPC(c, hipEventRecord(c->ev_fork, s));
-  if (do_tp) {
+  if (do_res) {
     HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
-    HIPC(c, launch_truepeak(W, sp, c->fork[0]));
+    if (split) {
+      HIPC(c, launch_mrfft_range(sp, 0, rb, c->fork[0]));
+      HIPC(c, launch_mrfft_range(sp, rb + 1, sp.n_res, c->fork[0]));
+    } else {
+      HIPC(c, launch_mrfft(sp, c->fork[0]));
+    }
     HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
   }
-  if (do_kw) {
-    HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_fork, 0));
-    HIPC(c, launch_kweight(W, kp, c->fork[1]));
+  if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
+  if (do_kw) HIPC(c, launch_kweight(W, kp, s));
+  if (meters) {
+    HIPC(c, hipEventRecord(c->ev_kw, s));
+    HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_kw, 0));
+    const int e = meters_enqueue(c, lufs, tp, n_frames, meters, c->fork[1]);
+    if (e) return e;
     HIPC(c, hipEventRecord(c->ev_join[1], c->fork[1]));
   }
-  HIPC(c, launch_mrfft(sp, s));
-  if (do_tp) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
-  if (do_kw) HIPC(c, hipStreamWaitEvent(s, c->ev_join[1], 0));
-  if (meters) return meters_enqueue(c, lufs, tp, n_frames, meters, s);
+  if (do_res && split) HIPC(c, launch_mrfft_range(sp, rb, rb + 1, s));
+  if (do_res) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
+  if (meters) HIPC(c, hipStreamWaitEvent(s, c->ev_join[1], 0));
   return 0;
 }
 
@@ -657,12 +713,18 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
     return fail(c, OMEGA_EHIP, "device %d: %s", device, hipGetErrorString(he));
   }
   c->stream = c->own;
+  if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
+    const int v = std::atoi(lay);
+    c->concurrent = v != 0;
+    c->layout = v;
+  }
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking);
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->fork[0], hipStreamNonBlocking);
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->fork[1], hipStreamNonBlocking);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_join[0], hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_join[1], hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_kw, hipEventDisableTiming);
   if (he != hipSuccess) {
     *out = c;
     return fail(c, OMEGA_EHIP, "streams/events: %s", hipGetErrorString(he));
@@ -688,7 +750,7 @@ void omega_destroy(omega_ctx* c) {
   }
   for (hipStream_t st : {c->cap, c->fork[0], c->fork[1]})
     if (st) (void)hipStreamDestroy(st);
-  for (hipEvent_t ev : {c->ev_fork, c->ev_join[0], c->ev_join[1]})
+  for (hipEvent_t ev : {c->ev_fork, c->ev_join[0], c->ev_join[1], c->ev_kw})
     if (ev) (void)hipEventDestroy(ev);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -704,7 +766,13 @@ int omega_set_stream(omega_ctx* c, void* s) {
 
 int omega_set_graphs(omega_ctx* c, int enable) {
   if (!c) return OMEGA_EINVAL;
-  c->use_graph = enable != 0;
+  c->use_graph = (enable & 1) != 0;
+  c->concurrent = (enable & 2) == 0;
+  for (auto& g : c->graphs) {
+    (void)hipGraphExecDestroy(g.exec);
+    (void)hipGraphDestroy(g.graph);
+  }
+  c->graphs.clear();
   return 0;
 }
 
@@ -720,6 +788,8 @@ int omega_meter_reset(omega_ctx* c) {
   for (int b = 0; b < 2; ++b) {
     HIPC(c, hipMemsetAsync(c->d_nl[b], 0, C * sizeof(int), c->stream));
     HIPC(c, hipMemsetAsync(c->d_nt[b], 0, C * sizeof(int), c->stream));
+    HIPC(c, hipMemsetAsync(c->d_ns[b], 0, C * sizeof(int), c->stream));
+    HIPC(c, hipMemsetAsync(c->d_t0[b], 0, C * sizeof(uint32_t), c->stream));
   }
   HIPC(c, hipStreamSynchronize(c->stream));
   return 0;
@@ -813,11 +883,7 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
       c->cur = cur0;  // capture advanced the parity; the replay below advances it for real
     }
     HIPC(c, hipGraphLaunch(exec, c->stream));
-    if (meters) {
-      const int64_t chunk = std::min<int64_t>(4096, kSortCapHost - c->HL);
-      const int64_t nchunks = (n_frames + chunk - 1) / chunk;
-      c->cur ^= (int)(nchunks & 1);
-    }
+    if (meters) c->cur ^= (int)(((n_frames + kChunkFrames - 1) / kChunkFrames) & 1);
     return 0;
   }
   e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->stream);

@@ -60,35 +60,34 @@ struct KWeightParams {
   int mode;                // 0: K-weighting, 3: Z (no filter, no gate: professional_meters.py:228-229)
 };
 
-struct MeterParams {
-  const float* lufs;   // [n_frames * C] batch instantaneous LUFS
-  const float* tp;     // [n_frames * C]
-  int64_t n_frames;
+// Meter aggregates (meters.hip): per-channel double-buffered state (in -> out) plus per-batch scratch.
+struct MeterPrepParams {
+  const float* lufs;    // [n_frames * C] batch instantaneous LUFS
+  const float* tp;      // [n_frames * C]
+  int64_t n_frames;     // <= 4096 per launch
   int C;
-  const float* hist_l;  // [C, HL] previous LUFS_inst values, oldest first
-  const float* hist_t;  // [C, HT] previous true-peak values
-  const int* n_hist_l;  // [C]
-  const int* n_hist_t;  // [C]
-  int HL, HT;           // capacities: integrated_len - 1, peak_len - 1
-  int mom_len, short_len, int_len, peak_len;
-  float gate;
-  double* out;          // [n_frames * C, 5]
-};
-
-struct MeterStateParams {
-  const float* lufs;
-  const float* tp;
-  int64_t n_frames;
-  int C;
-  const float* hist_l_in;
-  const float* hist_t_in;
+  const float* hist_l_in;  // [C, HL] last LUFS_inst values, time order
+  const float* hist_t_in;  // [C, HT] last TP values
   const int* n_l_in;
   const int* n_t_in;
+  const unsigned long long* skeys_in;  // [C, HL] gated keys of hist_l, sorted
+  const int* n_s_in;
+  const uint32_t* t0_in;  // absolute index of the batch's first frame
   float* hist_l_out;
   float* hist_t_out;
   int* n_l_out;
   int* n_t_out;
-  int HL, HT;
+  unsigned long long* skeys_out;
+  int* n_s_out;
+  uint32_t* t0_out;
+  int HL, HT;  // integrated_len - 1, peak_len - 1
+  int mom_len, short_len, int_len, peak_len;
+  float gate;
+  unsigned long long* union_keys;  // [C, 8192] scratch: sorted gated keys of history ++ batch
+  int* n_union;                    // [C]
+  int* gcount;                     // [C, 8193] gated-count prefix in time order
+  double* gsum;                    // [C, 8193] gated-sum prefix in time order
+  double* out;                     // [n_frames * C, 5]
 };
 
 struct BandParams {

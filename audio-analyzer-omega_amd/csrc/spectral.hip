@@ -274,10 +274,11 @@ __global__ __launch_bounds__(256) void combine_kernel(CombineParams p) {
     default: return hipErrorInvalidValue; \
   }
 
-// Resolution kernels, in resolution order (the combine owner protocol relies on it).
-hipError_t launch_mrfft(const SpectralParams& p, hipStream_t s) {
+// Resolution kernels for resolutions in [r0, r1), in resolution order (the combine owner protocol
+// relies on it whenever a target bin has several owners).
+hipError_t launch_mrfft_range(const SpectralParams& p, int r0, int r1, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
-  for (int r = 0; r < p.n_res; ++r) {
+  for (int r = r0; r < r1 && r < p.n_res; ++r) {
     if (!p.comb_out && !p.res[r].mag_out) continue;
 #define OMEGA_RES(K) \
   hipLaunchKernelGGL(mrfft_kernel<K>, grid, dim3(threads_for<K>()), K * sizeof(float2), s, p, r)
@@ -301,6 +302,8 @@ hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s) {
   }
   return hipGetLastError();
 }
+
+hipError_t launch_mrfft(const SpectralParams& p, hipStream_t s) { return launch_mrfft_range(p, 0, p.n_res, s); }
 
 hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s) {
   const hipError_t e = launch_mrfft(p, s);

@@ -61,9 +61,9 @@ def cfg2_input(frames=FRAMES, w=W, seed_l=0, seed_r=1):
 
 def kernel_time_ms(eng, xd, reps=20):
     """Average duration of the dominant kernel (the 8192-point true-peak kernel, one launch per batch)
-    from HIP events on the stream it is launched on (torch's current stream, bound to the context)."""
+    from HIP events on the stream it is launched on (torch's current stream, bound to the context:
+    omega_true_peak on device memory launches exactly that kernel there)."""
     from omega_gpu import _lib as L
-    import ctypes as Cc
     ncf = xd.numel() // W
     out = torch.empty(ncf, dtype=torch.float32, device=xd.device)
     lib = L.lib()

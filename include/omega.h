@@ -111,9 +111,11 @@ const char* omega_version(void);
  * stream). Contexts start on a private non-blocking stream. */
 int omega_set_stream(omega_ctx* ctx, void* hip_stream);
 /* Device-memory omega_process_frames calls are captured once per distinct argument set into a HIP
- * graph (three concurrent branches: resolution kernels / true peak / K-weighting, joined before the
- * meter aggregates) and replayed afterwards. Enabled by default; 0 launches directly. */
-int omega_set_graphs(omega_ctx* ctx, int enable);
+ * graph (three branches: resolution kernels / true peak / K-weighting, joined before the
+ * meter aggregates) and replayed afterwards. flags: bit 0 = use graphs (default on); bit 1 = run
+ * everything sequentially on one stream (default off: the latency-bound stages -- smaller resolutions,
+ * meter aggregates -- overlap the full-chip true-peak / K-weighting / largest-resolution kernels). */
+int omega_set_graphs(omega_ctx* ctx, int flags);
 int omega_synchronize(omega_ctx* ctx);
 
 /* The fused per-channel-frame hot path over n_frames x n_channels frames of W samples. */

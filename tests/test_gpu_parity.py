@@ -338,7 +338,7 @@ def test_graph_replay_matches_direct_launch():
     from omega_gpu import _lib as L
     x = torch.from_numpy(S.cfg2_batch(8)).cuda()
     outs = []
-    for graphs in (1, 0):
+    for graphs in (1, 2):  # graphs + concurrent branches vs direct sequential launches
         eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
         eng._check(L.lib().omega_set_graphs(eng._ctx, graphs))
         bufs = [{k: torch.empty(16, *s, dtype=d, device="cuda") for k, s, d in
