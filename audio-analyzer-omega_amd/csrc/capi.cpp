@@ -29,6 +29,8 @@ hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
 hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s);
+hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s);
+hipError_t launch_meter_query(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_bands(const BandParams& p, hipStream_t s);
 hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int hi, const double* mat, double* out,
                          hipStream_t s);
@@ -40,8 +42,7 @@ using namespace omega;
 namespace {
 
 constexpr double kPi = 3.14159265358979323846;
-constexpr int kUnionCapHost = 8192;  // meters.hip kUnionCap (4096 history + 4096 batch)
-constexpr int kChunkFrames = 4096;   // meters.hip kNewCap
+constexpr int kChunkFrames = kMeterChunk;
 
 struct DevBuf {
   void* p = nullptr;
@@ -153,7 +154,6 @@ struct omega_ctx {
   bool use_graph = true;
   bool concurrent = true;   // overlap the latency-bound stages (small FFTs, meters) with full-chip ones
   bool res_independent = false;  // no combine target has several owners: resolution kernels commute
-  int layout = 2;                // concurrent layouts (OMEGA_LAYOUT for A/B runs): 1 meters only, 2 full
   hipEvent_t ev_kw = nullptr;
   struct GraphEntry {
     std::vector<uint64_t> key;
@@ -167,10 +167,7 @@ struct omega_ctx {
   float2* d_rot = nullptr;
   float* d_win[kMaxRes] = {};
   float* d_wgt[kMaxRes] = {};
-  int* d_ent_t = nullptr;
-  int* d_ent_j = nullptr;
-  float* d_ent_frac = nullptr;
-  float* d_wsum = nullptr;
+  CombEnt* d_ent = nullptr;
   int ent_begin[kMaxRes] = {}, ent_end[kMaxRes] = {};
   std::map<int, BiquadTab*> kw_tabs;  // M -> device {hp, shelf}
   std::map<std::pair<int, int>, float*> windows;  // (m, kind) -> device window
@@ -190,8 +187,10 @@ struct omega_ctx {
   unsigned long long* d_skeys[2] = {};  // sorted gated history keys (double-buffered state)
   int* d_ns[2] = {};
   uint32_t* d_t0[2] = {};
-  unsigned long long* d_union = nullptr;  // per-batch scratch
-  int* d_nunion = nullptr;
+  float* d_core = nullptr;  // per-batch meter scratch
+  MeterExt* d_ext = nullptr;
+  int* d_ncore = nullptr;
+  int* d_next = nullptr;
   int* d_gcount = nullptr;
   double* d_gsum = nullptr;
   int HL = 0, HT = 0;
@@ -352,6 +351,7 @@ int validate(omega_ctx* c, const omega_config* cfg) {
 int build_spectral_tables(omega_ctx* c) {
   const omega_config& cfg = c->cfg;
   const double fs = cfg.sample_rate;
+  std::vector<std::vector<float>> wg(cfg.n_res);  // host copies of the weight tables
   for (int r = 0; r < cfg.n_res; ++r) {
     const omega_resolution& q = cfg.res[r];
     const int N = q.fft_size;
@@ -375,6 +375,7 @@ int build_spectral_tables(omega_ctx* c) {
     }
     e = upload(c, &c->d_wgt[r], w);
     if (e) return e;
+    wg[r] = std::move(w);
   }
   // combine plan (multi_resolution_fft.py:353-395)
   const int T = cfg.target_bins;
@@ -423,36 +424,34 @@ int build_spectral_tables(omega_ctx* c) {
   c->res_independent = true;
   for (int t = 0; t < T; ++t)
     if (own[t].size() > 1) c->res_independent = false;
-  std::vector<std::vector<int>> et(cfg.n_res), ej(cfg.n_res);
-  std::vector<std::vector<float>> ef(cfg.n_res);
-  std::vector<float> wsum(T, 0.f);
-  int first_res = -1;
-  for (int r = 0; r < cfg.n_res; ++r)
-    if (first_res < 0) first_res = r;
+  // per-resolution combine entries (see CombEnt): the interpolation of weighted magnitudes
+  // m_j + fr (m_{j+1} - m_j), m = |X| * wgt, times cw / sum of the target's owner weights
+  std::vector<std::vector<CombEnt>> er(cfg.n_res);
   for (int t = 0; t < T; ++t) {
     const auto& o = own[t];
-    for (const Ent& en : o) wsum[t] += (float)cfg.res[en.r].weight;
     if (o.empty()) {
-      et[first_res].push_back(t | (4 << 24));
-      ej[first_res].push_back(0);
-      ef[first_res].push_back(0.f);
+      er[0].push_back(CombEnt{t | (2 << 24), 0, 0.f, 0.f});
       continue;
     }
+    double ws = 0.0;
+    for (const Ent& en : o) ws += (double)(float)cfg.res[en.r].weight;
     for (size_t q = 0; q < o.size(); ++q) {
-      int mode = o.size() == 1 ? 0 : (q == 0 ? 1 : (q + 1 == o.size() ? 3 : 2));
-      et[o[q].r].push_back(t | (mode << 24));
-      ej[o[q].r].push_back(o[q].j);
-      ef[o[q].r].push_back(o[q].fr);
+      const Ent& en = o[q];
+      const double s = (double)(float)cfg.res[en.r].weight / ws;
+      const double fr = en.fr;
+      const int op = (q == 0 ? 0 : 1) << 24;
+      if (en.fr == 0.f && en.j == cfg.res[en.r].fft_size / 2)  // last bin: keep j + 1 in range
+        er[en.r].push_back(CombEnt{t | op, en.j - 1, 0.f, (float)(wg[en.r][en.j] * s)});
+      else
+        er[en.r].push_back(CombEnt{t | op, en.j, (float)((1.0 - fr) * wg[en.r][en.j] * s),
+                                   (float)(en.fr != 0.f ? fr * wg[en.r][en.j + 1] * s : 0.0)});
     }
   }
-  std::vector<int> at, aj;
-  std::vector<float> af;
+  std::vector<CombEnt> all;
   for (int r = 0; r < cfg.n_res; ++r) {
-    c->ent_begin[r] = (int)at.size();
-    at.insert(at.end(), et[r].begin(), et[r].end());
-    aj.insert(aj.end(), ej[r].begin(), ej[r].end());
-    af.insert(af.end(), ef[r].begin(), ef[r].end());
-    c->ent_end[r] = (int)at.size();
+    c->ent_begin[r] = (int)all.size();
+    all.insert(all.end(), er[r].begin(), er[r].end());
+    c->ent_end[r] = (int)all.size();
   }
   std::vector<int> ooff(1, 0), orj;
   std::vector<float> ofr;
@@ -466,10 +465,7 @@ int build_spectral_tables(omega_ctx* c) {
   int e = upload(c, &c->d_own_off, ooff);
   if (!e) e = upload(c, &c->d_own_rj, orj);
   if (!e) e = upload(c, &c->d_own_frac, ofr);
-  if (!e) e = upload(c, &c->d_ent_t, at);
-  if (!e) e = upload(c, &c->d_ent_j, aj);
-  if (!e) e = upload(c, &c->d_ent_frac, af);
-  if (!e) e = upload(c, &c->d_wsum, wsum);
+  if (!e) e = upload(c, &c->d_ent, all);
   if (e) return e;
   return get_rot(c, cfg.frame_size, &c->d_rot);
 }
@@ -491,10 +487,12 @@ int build_meter_state(omega_ctx* c) {
     if (!e) e = dalloc(c, &c->d_ns[b], C);
     if (!e) e = dalloc(c, &c->d_t0[b], C);
   }
-  if (!e) e = dalloc(c, &c->d_union, (size_t)C * kUnionCapHost);
-  if (!e) e = dalloc(c, &c->d_nunion, C);
-  if (!e) e = dalloc(c, &c->d_gcount, (size_t)C * (kUnionCapHost + 1));
-  if (!e) e = dalloc(c, &c->d_gsum, (size_t)C * (kUnionCapHost + 1));
+  if (!e) e = dalloc(c, &c->d_core, (size_t)C * kMeterSeqCap);
+  if (!e) e = dalloc(c, &c->d_ext, (size_t)C * kMeterSeqCap);
+  if (!e) e = dalloc(c, &c->d_ncore, C);
+  if (!e) e = dalloc(c, &c->d_next, C);
+  if (!e) e = dalloc(c, &c->d_gcount, (size_t)C * (kMeterSeqCap + 1));
+  if (!e) e = dalloc(c, &c->d_gsum, (size_t)C * (kMeterSeqCap + 1));
   if (e) return e;
   return omega_meter_reset(c);
 }
@@ -513,10 +511,7 @@ SpectralParams spectral_params(omega_ctx* c) {
     q.ent_end = c->ent_end[r];
     q.cw = (float)c->cfg.res[r].weight;
   }
-  p.ent_t = c->d_ent_t;
-  p.ent_j = c->d_ent_j;
-  p.ent_frac = c->d_ent_frac;
-  p.wsum = c->d_wsum;
+  p.ent = c->d_ent;
   p.T = c->cfg.target_bins;
   p.rot = c->d_rot;
   for (int l = 0; l < kMaxLog2; ++l) p.tw[l] = c->d_tw[l];
@@ -563,8 +558,10 @@ int finish_host(omega_ctx* c, const std::vector<HostOut>& outs) {
 
 // Meter aggregates over n_frames x C values, in chunks of at most kChunkFrames frames; each chunk
 // reads the state buffers `cur` and writes `cur ^ 1`.
+// tp_ready: when set, an event the true peaks of the batch wait on (the prep kernels only read the
+// LUFS_inst values, so they may start before it).
 int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_frames, double* out,
-                   hipStream_t stream) {
+                   hipStream_t stream, hipEvent_t tp_ready) {
   const int C = c->cfg.n_channels;
   for (int64_t f0 = 0; f0 < n_frames; f0 += kChunkFrames) {
     const int64_t nf = std::min<int64_t>(kChunkFrames, n_frames - f0);
@@ -595,22 +592,26 @@ int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_f
     p.int_len = c->cfg.integrated_len;
     p.peak_len = c->cfg.peak_len;
     p.gate = (float)c->cfg.gate_lufs;
-    p.union_keys = c->d_union;
-    p.n_union = c->d_nunion;
+    p.core = c->d_core;
+    p.ext = c->d_ext;
+    p.n_core = c->d_ncore;
+    p.n_ext = c->d_next;
     p.gcount = c->d_gcount;
     p.gsum = c->d_gsum;
     p.out = out + f0 * C * OMEGA_N_METERS;
-    HIPC(c, launch_meters(p, stream));
+    HIPC(c, launch_meter_prep(p, stream));
+    if (tp_ready && f0 == 0) HIPC(c, hipStreamWaitEvent(stream, tp_ready, 0));
+    HIPC(c, launch_meter_query(p, stream));
     c->cur = b;
   }
   return 0;
 }
 
 // The per-batch work. Sequential: resolution kernels, true peak, K-weighting, meters on `s`.
-// Concurrent (default): the full-chip kernels stay on `s` (true peak -> K-weighting -> the largest
-// resolution), the other resolution kernels run on fork[0] from the start (all of them, in order, when
-// combine targets have several owners), and the meter aggregates -- a few latency-bound workgroups --
-// run on fork[1] as soon as K-weighting is done; both branches join back into `s`.
+// Concurrent (default): true peak on fork[1] and the resolution kernels (in resolution order) on
+// fork[0] from the start; K-weighting and then the meter aggregates' prep kernel (it needs the batch's
+// LUFS_inst only) on `s`, whose query kernel then waits for the true peaks; both branches join back
+// into `s`.
 int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, int64_t n_frames,
                    const float* lufs, const float* tp, double* meters, hipStream_t s) {
   const bool do_tp = sp.tp_out != nullptr, do_kw = kp.lufs_out || kp.weighted_out;
@@ -620,49 +621,26 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
     if (do_res) HIPC(c, launch_mrfft(sp, s));
     if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
     if (do_kw) HIPC(c, launch_kweight(W, kp, s));
-    return meters ? meters_enqueue(c, lufs, tp, n_frames, meters, s) : 0;
-  }
-  int rb = 0;
-  for (int r = 1; r < sp.n_res; ++r)
-    if (sp.res[r].n > sp.res[rb].n) rb = r;
-  const bool split = c->res_independent;
-  if (c->layout == 1) {  // only the meter aggregates on a side branch
-    if (do_res) HIPC(c, launch_mrfft(sp, s));
-    if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
-    if (do_kw) HIPC(c, launch_kweight(W, kp, s));
-    if (meters) {
-      HIPC(c, hipEventRecord(c->ev_kw, s));
-      HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_kw, 0));
-      const int e = meters_enqueue(c, lufs, tp, n_frames, meters, c->fork[1]);
-      if (e) return e;
-      HIPC(c, hipEventRecord(c->ev_join[1], c->fork[1]));
-      HIPC(c, hipStreamWaitEvent(s, c->ev_join[1], 0));
-    }
-    return 0;
+    return meters ? meters_enqueue(c, lufs, tp, n_frames, meters, s, nullptr) : 0;
   }
   HIPC(c, hipEventRecord(c->ev_fork, s));
-  if (do_res) {
-    HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
-    if (split) {
-      HIPC(c, launch_mrfft_range(sp, 0, rb, c->fork[0]));
-      HIPC(c, launch_mrfft_range(sp, rb + 1, sp.n_res, c->fork[0]));
-    } else {
-      HIPC(c, launch_mrfft(sp, c->fork[0]));
-    }
-    HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
-  }
-  if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
-  if (do_kw) HIPC(c, launch_kweight(W, kp, s));
-  if (meters) {
-    HIPC(c, hipEventRecord(c->ev_kw, s));
-    HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_kw, 0));
-    const int e = meters_enqueue(c, lufs, tp, n_frames, meters, c->fork[1]);
-    if (e) return e;
+  if (do_tp) {
+    HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_fork, 0));
+    HIPC(c, launch_truepeak(W, sp, c->fork[1]));
     HIPC(c, hipEventRecord(c->ev_join[1], c->fork[1]));
   }
-  if (do_res && split) HIPC(c, launch_mrfft_range(sp, rb, rb + 1, s));
+  if (do_res) {
+    HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
+    HIPC(c, launch_mrfft(sp, c->fork[0]));
+    HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
+  }
+  if (do_kw) HIPC(c, launch_kweight(W, kp, s));
+  if (meters) {
+    const int e = meters_enqueue(c, lufs, tp, n_frames, meters, s, do_tp ? c->ev_join[1] : nullptr);
+    if (e) return e;
+  }
+  if (do_tp) HIPC(c, hipStreamWaitEvent(s, c->ev_join[1], 0));
   if (do_res) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
-  if (meters) HIPC(c, hipStreamWaitEvent(s, c->ev_join[1], 0));
   return 0;
 }
 
@@ -716,7 +694,6 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
     const int v = std::atoi(lay);
     c->concurrent = v != 0;
-    c->layout = v;
   }
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking);
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->fork[0], hipStreamNonBlocking);
@@ -1012,7 +989,7 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
     if (!e) e = stage_out(c, 4, meters, ncf * 5, outs, &dm);
     if (e) return e;
   }
-  e = meters_enqueue(c, dl, dt, n_frames, dm, c->stream);
+  e = meters_enqueue(c, dl, dt, n_frames, dm, c->stream, nullptr);
   if (e) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;

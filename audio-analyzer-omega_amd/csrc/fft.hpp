@@ -112,25 +112,32 @@ __device__ __forceinline__ int swz(int i) {
   }
 }
 
+// Per-pass twiddle bases held in registers: pass I (stride NS > 1) needs w = tw[(j mod NS) K/(NS R)]
+// for its one butterfly j = tid. Loaded once, up front, with the frame's first global loads (one
+// memory latency for the whole transform instead of one per pass), and reused by every transform a
+// kernel runs with the same plan.
+template <int NP>
+struct TwReg {
+  float2 w[NP > 0 ? NP : 1];
+  // Make the values opaque to the optimiser: inside a loop that runs several transforms this stops
+  // LICM from hoisting every pass's twiddle powers (w^2 .. w^(R-1)) and pinning them in VGPRs.
+  __device__ __forceinline__ void launder() {
+    static_for<0, (NP > 0 ? NP : 1)>([&](auto i) { asm volatile("" : "+v"(w[i].x), "+v"(w[i].y)); });
+  }
+};
+
 // One Stockham pass over K points with NTH threads: butterfly j in [0, K/R) reads logical elements
 // j + r*K/R (r < R) through `load`, multiplies element r by w^(r*k) with k = j mod NS and
 // w = exp(-2 pi i / (NS*R)), DFTs, and hands output m to `store` at logical index
-// (j/NS)*NS*R + k + m*NS. The twiddle base is fetched before the loads (its global-memory latency
-// overlaps the LDS reads and the barrier) and its powers are formed by a multiply chain (two live
-// registers instead of R). SYNC_MID: loads and stores hit the same LDS buffer in place, so a
-// barrier separates all reads from all writes.
+// (j/NS)*NS*R + k + m*NS. w1: the preloaded base w^k of this thread's butterfly (passes with NS > 1
+// have one butterfly per thread); its powers are formed by a multiply chain. SYNC_MID: loads and
+// stores hit the same LDS buffer in place, so a barrier separates all reads from all writes.
 template <int K, int R, int NS, int NTH, bool SYNC_MID, class Load, class Store>
-__device__ __forceinline__ void fft_pass(const float2* __restrict__ tw, int tid, Load&& load, Store&& store) {
+__device__ __forceinline__ void fft_pass(float2 w1, int tid, Load&& load, Store&& store) {
   constexpr int NB = K / R;
   constexpr int B = (NB + NTH - 1) / NTH;
+  static_assert(NS == 1 || B == 1, "twiddled passes: one butterfly per thread");
   float2 v[B][R];
-  float2 w1[B];
-  static_for<0, B>([&](auto b) {
-    const int j = tid + b * NTH;
-    if constexpr (NS > 1) {
-      if (NB % NTH == 0 || j < NB) w1[b] = tw[(j & (NS - 1)) * (K / (NS * R))];
-    }
-  });
   static_for<0, B>([&](auto b) {
     const int j = tid + b * NTH;
     if (NB % NTH == 0 || j < NB) static_for<0, R>([&](auto r) { v[b][r] = load(j + r * NB); });
@@ -141,10 +148,10 @@ __device__ __forceinline__ void fft_pass(const float2* __restrict__ tw, int tid,
     if (NB % NTH == 0 || j < NB) {
       const int k = j & (NS - 1);
       if constexpr (NS > 1) {
-        float2 w = w1[b];
+        float2 w = w1;
         static_for<1, R>([&](auto r) {
           v[b][r] = cmul(v[b][r], w);
-          if constexpr (r + 1 < R) w = cmul(w, w1[b]);
+          if constexpr (r + 1 < R) w = cmul(w, w1);
         });
       }
       dft_dif<R>(v[b]);
@@ -154,23 +161,34 @@ __device__ __forceinline__ void fft_pass(const float2* __restrict__ tw, int tid,
   });
 }
 
-// Radix plan R0, R1, ... applied in order with NS = product of the radices before each pass.
-// FIRST/LAST: whether the first pass loads through `first` (e.g. straight from global memory) and
-// the last pass stores through `last` (e.g. a register-side reduction) instead of the LDS buffer.
-template <int K, int NTH, int NS, int PNS, int PR, int... Rs>
+// Radix plan R0, R1, ... applied in order with NS = product of the radices before each pass; I is
+// the pass index. FIRST/LAST: whether the first pass loads through `first` (e.g. straight from
+// global memory) and the last pass stores through `last` (e.g. a register-side reduction) instead
+// of the LDS buffer.
+template <int K, int NTH, int I, int NS, int PNS, int PR, int... Rs>
 struct StockhamChain;
-template <int K, int NTH, int NS, int PNS, int PR>
-struct StockhamChain<K, NTH, NS, PNS, PR> {
-  template <bool FIRST, bool LAST, class F, class G>
-  static __device__ __forceinline__ void run(float2*, const float2*, int, F&&, G&&) {}
+template <int K, int NTH, int I, int NS, int PNS, int PR>
+struct StockhamChain<K, NTH, I, NS, PNS, PR> {
+  template <class TW>
+  static __device__ __forceinline__ void load_tw(const float2*, int, TW&) {}
+  template <bool FIRST, bool LAST, class TW, class F, class G>
+  static __device__ __forceinline__ void run(float2*, const TW&, int, F&&, G&&) {}
   static __device__ __forceinline__ int out(int i) { return swz<PNS, PR>(i); }
 };
-template <int K, int NTH, int NS, int PNS, int PR, int R, int... Rs>
-struct StockhamChain<K, NTH, NS, PNS, PR, R, Rs...> {
-  using Next = StockhamChain<K, NTH, NS * R, NS, R, Rs...>;
+template <int K, int NTH, int I, int NS, int PNS, int PR, int R, int... Rs>
+struct StockhamChain<K, NTH, I, NS, PNS, PR, R, Rs...> {
+  using Next = StockhamChain<K, NTH, I + 1, NS * R, NS, R, Rs...>;
   static constexpr bool kLastPass = sizeof...(Rs) == 0;
-  template <bool FIRST, bool LAST, class F, class G>
-  static __device__ __forceinline__ void run(float2* buf, const float2* tw, int t, F&& first, G&& last) {
+  template <class TW>
+  static __device__ __forceinline__ void load_tw(const float2* __restrict__ tw, int t, TW& w) {
+    w.w[I] = make_float2(1.f, 0.f);
+    if constexpr (NS > 1) {
+      if ((K / R) % NTH == 0 || t < K / R) w.w[I] = tw[(t & (NS - 1)) * (K / (NS * R))];
+    }
+    Next::load_tw(tw, t, w);
+  }
+  template <bool FIRST, bool LAST, class TW, class F, class G>
+  static __device__ __forceinline__ void run(float2* buf, const TW& w, int t, F&& first, G&& last) {
     auto lds_load = [&](int i) { return buf[swz<PNS, PR>(i)]; };
     auto lds_store = [&](int i, float2 v) { buf[swz<NS, R>(i)] = v; };
     constexpr bool in_global = FIRST && NS == 1;
@@ -178,41 +196,48 @@ struct StockhamChain<K, NTH, NS, PNS, PR, R, Rs...> {
     // in place in LDS needs the mid-pass barrier; a global-source or register-sink pass does not
     constexpr bool sync_mid = !in_global && !out_regs;
     if constexpr (in_global && out_regs)
-      fft_pass<K, R, NS, NTH, false>(tw, t, first, last);
+      fft_pass<K, R, NS, NTH, false>(w.w[I], t, first, last);
     else if constexpr (in_global)
-      fft_pass<K, R, NS, NTH, false>(tw, t, first, lds_store);
+      fft_pass<K, R, NS, NTH, false>(w.w[I], t, first, lds_store);
     else if constexpr (out_regs)
-      fft_pass<K, R, NS, NTH, false>(tw, t, lds_load, last);
+      fft_pass<K, R, NS, NTH, false>(w.w[I], t, lds_load, last);
     else
-      fft_pass<K, R, NS, NTH, sync_mid>(tw, t, lds_load, lds_store);
+      fft_pass<K, R, NS, NTH, sync_mid>(w.w[I], t, lds_load, lds_store);
     if constexpr (!out_regs) __syncthreads();  // results visible to the next pass / the caller
-    Next::template run<FIRST, LAST>(buf, tw, t, first, last);
+    Next::template run<FIRST, LAST>(buf, w, t, first, last);
   }
   static __device__ __forceinline__ int out(int i) { return Next::out(i); }
 };
 
 // Forward complex FFT of K points with NTH threads. Natural order in (identity swizzle) and out
-// (element i at buf[out(i)]). tw: exp(-2 pi i m / K), m < K. run(): input already in LDS and the
-// caller synchronised; run_from(first): the first pass reads logical element i as first(i) (no LDS
-// write of the input; the caller must make sure no one still reads buf); run_to(last): the last pass
-// hands outputs to last(i, v) instead of LDS (the caller synchronises before reusing buf).
+// (element i at buf[out(i)]). Twiddles: Tw from load_tw(tw) with tw = exp(-2 pi i m / K), m < K.
+// run(): input already in LDS and the caller synchronised; run_from(first): the first pass reads
+// logical element i as first(i) (no LDS write of the input; the caller must make sure no one still
+// reads buf); run_to(last): the last pass hands outputs to last(i, v) instead of LDS (the caller
+// synchronises before reusing buf).
 template <int K, int NTH, int... Rs>
 struct FFTPlan {
-  using Chain = StockhamChain<K, NTH, 1, 0, 1, Rs...>;
-  static __device__ __forceinline__ void run(float2* b, const float2* tw, int t) {
+  using Chain = StockhamChain<K, NTH, 0, 1, 0, 1, Rs...>;
+  using Tw = TwReg<sizeof...(Rs)>;
+  static __device__ __forceinline__ Tw load_tw(const float2* __restrict__ tw, int t) {
+    Tw w;
+    Chain::load_tw(tw, t, w);
+    return w;
+  }
+  static __device__ __forceinline__ void run(float2* b, const Tw& w, int t) {
     auto none = [](int) { return make_float2(0.f, 0.f); };
     auto sink = [](int, float2) {};
-    Chain::template run<false, false>(b, tw, t, none, sink);
+    Chain::template run<false, false>(b, w, t, none, sink);
   }
   template <class F>
-  static __device__ __forceinline__ void run_from(float2* b, const float2* tw, int t, F&& first) {
+  static __device__ __forceinline__ void run_from(float2* b, const Tw& w, int t, F&& first) {
     auto sink = [](int, float2) {};
-    Chain::template run<true, false>(b, tw, t, first, sink);
+    Chain::template run<true, false>(b, w, t, first, sink);
   }
   template <class G>
-  static __device__ __forceinline__ void run_to(float2* b, const float2* tw, int t, G&& last) {
+  static __device__ __forceinline__ void run_to(float2* b, const Tw& w, int t, G&& last) {
     auto none = [](int) { return make_float2(0.f, 0.f); };
-    Chain::template run<false, true>(b, tw, t, none, last);
+    Chain::template run<false, true>(b, w, t, none, last);
   }
   static __device__ __forceinline__ int out(int i) { return Chain::out(i); }
 };
@@ -225,6 +250,9 @@ constexpr int threads_for() { return K / 16 < 64 ? 64 : (K / 16 > 512 ? 512 : K 
 template <int K, int NTH>
 struct BlockFFTPlan;
 template <int NTH> struct BlockFFTPlan<8192, NTH> { using type = FFTPlan<8192, NTH, 2, 16, 16, 16>; };
+// 1024 threads, radix 8 (one butterfly per thread per pass): the true-peak kernel's plan, where the
+// held spectrum makes radix-16 registers too costly for more than 2 waves per SIMD
+template <> struct BlockFFTPlan<8192, 1024> { using type = FFTPlan<8192, 1024, 2, 8, 8, 8, 8>; };
 template <int NTH> struct BlockFFTPlan<4096, NTH> { using type = FFTPlan<4096, NTH, 16, 16, 16>; };
 template <int NTH> struct BlockFFTPlan<2048, NTH> { using type = FFTPlan<2048, NTH, 8, 16, 16>; };
 template <int NTH> struct BlockFFTPlan<1024, NTH> { using type = FFTPlan<1024, NTH, 4, 16, 16>; };

@@ -9,23 +9,27 @@
 // Device state per channel (double-buffered): the last 3599 LUFS_inst and 59 TP values in time order,
 // the gated ones among those 3599 kept SORTED as 64-bit keys (order-preserving value key << 32 |
 // absolute frame index), and the absolute index of the next frame.
-// Per batch:
-//   meter_prep_kernel  (one 1024-thread workgroup per channel): bitonic-sort only the batch's gated
-//     values, merge them with the sorted history by rank (merge-path positions: own index + binary-
-//     search rank in the other list) into the union list the queries read, write the next sorted
-//     history (dropping keys older than the window) the same way, prefix-count/sum the gated values in
-//     time order, and roll the time-ordered histories.
-//   meter_query_kernel (one wave per frame): gated count and sum from the time-order prefixes, then one
-//     sweep over the sorted union with wave ballots finds the four order statistics of the frame's
-//     window (its index range) -- no per-frame sort.
+//
+// The windows of one batch's frames slide by one frame each, so they share a core: the frames
+// [lo_{F-1}, hi_0] that lie in every window. Per batch:
+//   meter_prep_kernel  (one 1024-thread workgroup per channel): sort the batch's gated keys, merge
+//     them with the sorted history by rank (merge-path positions: own index + binary-search rank in the
+//     other list), split the merged list into the sorted CORE values and the sorted EXTRA values
+//     (gated values outside the core, at most 2(F-1)), each extra tagged with its frame index and the
+//     number of core values below it; write the next sorted history (dropping keys older than the
+//     window) the same way; prefix-count/sum the gated values in time order; roll the histories.
+//   meter_query_kernel (one wave per frame): gated count and sum from the time-order prefixes. The
+//     frame's gated window is core + the extras inside its window; extra j (in value order among
+//     those) sits at merged rank j + its core count, so the k-th order statistic is either such an
+//     extra or core[k - #extras ranked below k] -- a pass over the extras, no per-frame sort.
 #include "fft.hpp"
 #include "params.hpp"
 
 namespace omega {
 
-constexpr int kNewCap = 4096;   // batch chunk (frames) per launch; the host splits longer batches
-constexpr int kHistCap = 4096;  // >= integrated_len - 1
-constexpr int kUnionCap = kNewCap + kHistCap;
+constexpr int kNewCap = kMeterChunk;
+constexpr int kHistCap = kMeterHistCap;
+constexpr int kSeqCap = kMeterSeqCap;
 
 __device__ __forceinline__ uint32_t fkey(float v) {
   const uint32_t u = __float_as_uint(v);
@@ -68,96 +72,164 @@ __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int tid, int& e
   excl = base + incl - v;
   return tot;
 }
-__device__ __forceinline__ double block_excl_scan_d(double v, double* wsum, int tid, double& excl) {
+
+// two exclusive int scans and one double scan in one pass (1024 threads)
+__device__ __forceinline__ void block_excl_scan3(int a, int b, double d, int* wsa, int* wsb, double* wsd, int tid,
+                                                 int& ea, int& eb, double& ed) {
   const int lane = tid & 63, wv = tid >> 6;
-  double incl = v;
+  int ia = a, ib = b;
+  double id = d;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const double o = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += o;
+  for (int s = 1; s < 64; s <<= 1) {
+    const int oa = __shfl_up(ia, s, 64), ob = __shfl_up(ib, s, 64);
+    const double od = __shfl_up(id, s, 64);
+    if (lane >= s) {
+      ia += oa;
+      ib += ob;
+      id += od;
+    }
   }
-  if (lane == 63) wsum[wv] = incl;
-  __syncthreads();
-  double base = 0, tot = 0;
-  for (int w = 0; w < 16; ++w) {
-    base += w < wv ? wsum[w] : 0.0;
-    tot += wsum[w];
+  if (lane == 63) {
+    wsa[wv] = ia;
+    wsb[wv] = ib;
+    wsd[wv] = id;
   }
   __syncthreads();
-  excl = base + incl - v;
-  return tot;
+  int ba = 0, bb = 0;
+  double bd = 0.0;
+  for (int w = 0; w < wv; ++w) {
+    ba += wsa[w];
+    bb += wsb[w];
+    bd += wsd[w];
+  }
+  __syncthreads();
+  ea = ba + ia - a;
+  eb = bb + ib - b;
+  ed = bd + id - d;
 }
 
+// Window of batch frame f as absolute frame indices [lo, hi] (hi = T0 + f).
+__device__ __forceinline__ uint32_t window_lo(uint32_t T0, int nh, int64_t f, int int_len) {
+  const int64_t n = nh + f + 1;
+  return T0 - (uint32_t)nh + (uint32_t)(n - min<int64_t>(int_len, n));
+}
+
+// The stream's LUFS_inst sequence over [T0 - nh, T0 + F) lives in LDS (V); every global input is
+// fetched once, up front.
 __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
-  __shared__ unsigned long long B[kNewCap];
-  __shared__ unsigned long long A[kHistCap];
-  __shared__ int kp[kHistCap];  // exclusive prefix of kept flags over A (key order)
-  __shared__ int kb[kNewCap];   // exclusive prefix of kept flags over B (key order)
-  __shared__ int wsi[16];
+  __shared__ unsigned long long B[kNewCap];   // the batch's gated keys, sorted
+  __shared__ unsigned long long A[kHistCap];  // the history's gated keys, sorted
+  __shared__ unsigned long long U[kSeqCap];   // A merged with B
+  __shared__ float V[kSeqCap];                // time-ordered LUFS_inst, history ++ batch
+  __shared__ int kp[kHistCap];                // exclusive prefix of kept flags over A (key order)
+  __shared__ int kb[kNewCap];                 // exclusive prefix of kept flags over B (key order)
+  __shared__ int wsa[16], wsb[16];
   __shared__ double wsd[16];
   const int c = blockIdx.x, tid = threadIdx.x;
   const int C = p.C, F = (int)p.n_frames;
   const uint32_t T0 = p.t0_in[c];
-  const int nh = p.n_l_in[c], ns = p.n_s_in[c], nt = p.n_t_in[c];
+  const int nh = p.n_l_in[c], ns = p.n_s_in[c];
+  const int L = nh + F;
   const int64_t thr = (int64_t)T0 + F - p.HL;  // oldest absolute index the next batch's windows reach
-  // 1) the batch's gated keys, sorted
+  const float gate = p.gate;
+  // 1) stage the sequence and the sorted history (loads of a thread issued together)
+#pragma unroll
+  for (int q = 0; q < kSeqCap / 1024; ++q) {
+    const int u = q * 1024 + tid;
+    if (u < L) V[u] = u < nh ? p.hist_l_in[(int64_t)c * p.HL + u] : p.lufs[(int64_t)(u - nh) * C + c];
+  }
+#pragma unroll
+  for (int q = 0; q < kHistCap / 1024; ++q) {
+    const int i = q * 1024 + tid;
+    if (i < ns) A[i] = p.skeys_in[(int64_t)c * p.HL + i];
+  }
+  __syncthreads();
+  auto bkey = [&](int f) -> unsigned long long {
+    const float v = V[nh + f];
+    return v > gate ? ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)f) : ~0ull;
+  };
+  // 2) sort the batch's gated keys (distinct: they carry the frame index). Up to 1024 frames: rank
+  // sort, P threads per key (adjacent lanes) each counting the smaller keys of a 1/P slice; beyond:
+  // bitonic.
+  int Gn;
   int Fp = 1;
   while (Fp < F) Fp <<= 1;
-  for (int f = tid; f < Fp; f += 1024) {
-    unsigned long long k = ~0ull;
-    if (f < F) {
-      const float v = p.lufs[(int64_t)f * C + c];
-      if (v > p.gate) k = ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)f);
+  if (Fp <= 1024) {
+    const int P = min(64, 1024 / Fp);
+    const int f = tid / P, part = tid % P;
+    const int len = (F + P - 1) / P, g0 = part * len, g1 = min(F, g0 + len);
+    const unsigned long long k = f < F ? bkey(f) : ~0ull;
+    int rank = 0;
+    if (k != ~0ull) {
+#pragma unroll 8
+      for (int g = g0; g < g1; ++g) rank += bkey(g) < k;
     }
-    B[f] = k;
-  }
-  for (int i = tid; i < ns; i += 1024) A[i] = p.skeys_in[(int64_t)c * p.HL + i];
-  __syncthreads();
-  for (int k = 2; k <= Fp; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < Fp; i += 1024) {
-        const int l = i ^ j;
-        if (l > i) {
-          const unsigned long long a = B[i], b = B[l];
-          if ((a > b) == ((i & k) == 0)) {
-            B[i] = b;
-            B[l] = a;
+    for (int o = 1; o < P; o <<= 1) rank += __shfl_xor(rank, o, 64);
+    int dummy;
+    Gn = block_excl_scan(part == 0 && k != ~0ull ? 1 : 0, wsa, tid, dummy);
+    if (part == 0 && k != ~0ull) B[rank] = k;
+  } else {
+    for (int f = tid; f < Fp; f += 1024) B[f] = f < F ? bkey(f) : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= Fp; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < Fp; i += 1024) {
+          const int l = i ^ j;
+          if (l > i) {
+            const unsigned long long a = B[i], b = B[l];
+            if ((a > b) == ((i & k) == 0)) {
+              B[i] = b;
+              B[l] = a;
+            }
           }
         }
+        __syncthreads();
       }
-      __syncthreads();
+    }
+    int gn_part = 0;
+    for (int i = tid; i < Fp; i += 1024) gn_part += B[i] != ~0ull;
+    int dummy;
+    Gn = block_excl_scan(gn_part, wsa, tid, dummy);
+  }
+  // 3) kept flags (absolute index >= thr) and their key-order prefixes, for A and B
+  constexpr int PA = kHistCap / 1024, PB = kNewCap / 1024;
+  int Ka, Kb;
+  {
+    int fa[PA], fb[PB], sa = 0, sb = 0;
+#pragma unroll
+    for (int q = 0; q < PA; ++q) {
+      const int i = tid * PA + q;
+      fa[q] = i < ns && (int64_t)(uint32_t)A[i] >= thr;
+      sa += fa[q];
+    }
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int i = tid * PB + q;
+      fb[q] = i < Gn && (int64_t)(uint32_t)B[i] >= thr;
+      sb += fb[q];
+    }
+    int ea, eb;
+    double ed;
+    block_excl_scan3(sa, sb, 0.0, wsa, wsb, wsd, tid, ea, eb, ed);
+#pragma unroll
+    for (int q = 0; q < PA; ++q) {
+      kp[tid * PA + q] = ea;
+      ea += fa[q];
+    }
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      kb[tid * PB + q] = eb;
+      eb += fb[q];
+    }
+    if (tid == 1023) {
+      wsa[0] = ea;  // totals, read after the barrier below
+      wsb[0] = eb;
     }
   }
-  // gated count of the batch = first sentinel position
-  int gn_part = 0;
-  for (int i = tid; i < Fp; i += 1024) gn_part += B[i] != ~0ull;
-  int dummy;
-  const int Gn = block_excl_scan(gn_part, wsi, tid, dummy);
-  // 2) kept flags (absolute index >= thr) and their key-order prefixes, for A (4 per thread) and B
-  constexpr int PER = kHistCap / 1024;
-  int fa[PER], fb[PER], sa = 0, sb = 0;
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int i = tid * PER + q;
-    fa[q] = i < ns && (int64_t)(uint32_t)A[i] >= thr;
-    fb[q] = i < Gn && (int64_t)(uint32_t)B[i] >= thr;
-    sa += fa[q];
-    sb += fb[q];
-  }
-  int ea, eb;
-  const int Ka = block_excl_scan(sa, wsi, tid, ea);
-  const int Kb = block_excl_scan(sb, wsi, tid, eb);
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int i = tid * PER + q;
-    kp[i] = ea;
-    kb[i] = eb;
-    ea += fa[q];
-    eb += fb[q];
-  }
   __syncthreads();
-  // 3) union (all of A and B) for the queries, and the next sorted history (kept ones), by rank
-  unsigned long long* U = p.union_keys + (int64_t)c * kUnionCap;
+  Ka = wsa[0];
+  Kb = wsb[0];
+  // 4) the merged list U, and the next sorted history (kept ones), by rank
   unsigned long long* S = p.skeys_out + (int64_t)c * p.HL;
   for (int i = tid; i < ns; i += 1024) {
     const int r = lower_rank(B, Gn, A[i]);
@@ -169,50 +241,88 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     U[j + r] = B[j];
     if ((int64_t)(uint32_t)B[j] >= thr) S[kb[j] + (r < ns ? kp[r] : Ka)] = B[j];
   }
-  // 4) gated count / sum prefixes in time order over [T0 - nh, T0 + F)
-  const int L = nh + F;
-  int* gp = p.gcount + (int64_t)c * (kUnionCap + 1);
-  double* gsum = p.gsum + (int64_t)c * (kUnionCap + 1);
-  int carry_i = 0;
-  double carry_d = 0.0;
-  for (int base = 0; base < L; base += 1024) {
-    const int u = base + tid;
-    float v = -INFINITY;
-    if (u < L) v = u < nh ? p.hist_l_in[(int64_t)c * p.HL + u] : p.lufs[(int64_t)(u - nh) * C + c];
-    const bool g = u < L && v > p.gate;
-    int ei;
-    double ed;
-    const int ti = block_excl_scan(g ? 1 : 0, wsi, tid, ei);
-    const double td = block_excl_scan_d(g ? (double)v : 0.0, wsd, tid, ed);
-    if (u < L) {
-      gp[u] = carry_i + ei;
-      gsum[u] = carry_d + ed;
+  __syncthreads();
+  // 5) split U into core / extra (a contiguous run per thread), and the gated count / sum prefixes
+  // in time order over [T0 - nh, T0 + F) (a contiguous run of V per thread)
+  const int G = ns + Gn;
+  const uint32_t clo = window_lo(T0, nh, F - 1, p.int_len), chi = T0;
+  const bool has_core = (int32_t)(chi - clo) >= 0;
+  auto in_core = [&](unsigned long long k) { return has_core && (uint32_t)((uint32_t)k - clo) <= chi - clo; };
+  const int pu = (G + 1023) / 1024, u0 = tid * pu;
+  const int pv = (L + 1023) / 1024, v0 = tid * pv;
+  int cc = 0, ce = 0, gi = 0;
+  double gd = 0.0;
+  for (int q = 0; q < pu; ++q) {
+    const int u = u0 + q;
+    if (u < G) {
+      const bool core = in_core(U[u]);
+      cc += core;
+      ce += !core;
     }
-    carry_i += ti;
-    carry_d += td;
+  }
+  for (int q = 0; q < pv; ++q) {
+    const int u = v0 + q;
+    if (u < L && V[u] > gate) {
+      ++gi;
+      gd += (double)V[u];
+    }
+  }
+  int ec, ee;
+  double ed;
+  block_excl_scan3(cc, ce, gd, wsa, wsb, wsd, tid, ec, ee, ed);
+  int eg, dummy_b;
+  double dummy_d;
+  block_excl_scan3(gi, 0, 0.0, wsa, wsb, wsd, tid, eg, dummy_b, dummy_d);
+  float* core = p.core + (int64_t)c * kSeqCap;
+  MeterExt* ext = p.ext + (int64_t)c * kSeqCap;
+  for (int q = 0; q < pu; ++q) {
+    const int u = u0 + q;
+    if (u < G) {
+      const unsigned long long k = U[u];
+      if (in_core(k)) {
+        core[ec++] = unkey((uint32_t)(k >> 32));
+      } else {
+        ext[ee++] = MeterExt{unkey((uint32_t)(k >> 32)), (uint32_t)k, ec, 0};
+      }
+    }
+  }
+  int* gp = p.gcount + (int64_t)c * (kSeqCap + 1);
+  double* gsum = p.gsum + (int64_t)c * (kSeqCap + 1);
+  for (int q = 0; q < pv; ++q) {
+    const int u = v0 + q;
+    if (u < L) {
+      gp[u] = eg;
+      gsum[u] = ed;
+      if (V[u] > gate) {
+        ++eg;
+        ed += (double)V[u];
+      }
+    }
+  }
+  if (v0 < L && v0 + pv >= L) {  // the run that ends the sequence holds the totals
+    gp[L] = eg;
+    gsum[L] = ed;
+  }
+  if (u0 < G && u0 + pu >= G) {
+    p.n_core[c] = ec;
+    p.n_ext[c] = ee;
   }
   if (tid == 0) {
-    gp[L] = carry_i;
-    gsum[L] = carry_d;
-    p.n_union[c] = ns + Gn;
+    if (L == 0) {
+      gp[0] = 0;
+      gsum[0] = 0.0;
+    }
+    if (G == 0) {
+      p.n_core[c] = 0;
+      p.n_ext[c] = 0;
+    }
     p.n_s_out[c] = Ka + Kb;
     p.t0_out[c] = T0 + (uint32_t)F;
   }
-  // 5) time-ordered histories for the next batch
-  const int64_t tl = (int64_t)nh + F, tt = (int64_t)nt + F;
-  const int klen = (int)min<int64_t>(p.HL, tl), ktl = (int)min<int64_t>(p.HT, tt);
-  for (int i = tid; i < klen; i += 1024) {
-    const int64_t j = tl - klen + i;
-    p.hist_l_out[(int64_t)c * p.HL + i] = j < nh ? p.hist_l_in[(int64_t)c * p.HL + j] : p.lufs[(j - nh) * C + c];
-  }
-  for (int i = tid; i < ktl; i += 1024) {
-    const int64_t j = tt - ktl + i;
-    p.hist_t_out[(int64_t)c * p.HT + i] = j < nt ? p.hist_t_in[(int64_t)c * p.HT + j] : p.tp[(j - nt) * C + c];
-  }
-  if (tid == 0) {
-    p.n_l_out[c] = klen;
-    p.n_t_out[c] = ktl;
-  }
+  // 6) time-ordered LUFS history for the next batch (the TP history rolls in meter_query_kernel)
+  const int klen = min(p.HL, L);
+  for (int i = tid; i < klen; i += 1024) p.hist_l_out[(int64_t)c * p.HL + i] = V[L - klen + i];
+  if (tid == 0) p.n_l_out[c] = klen;
 }
 
 __device__ __forceinline__ double lerp_pct(double a, double b, double gamma) {
@@ -225,14 +335,25 @@ __device__ __forceinline__ float seq_at(const float* hist, const float* batch, i
   return i < nh ? hist[(int64_t)c * HC + i] : batch[(i - nh) * C + c];
 }
 
-// One wave per output (f, c).
+// One wave per output (f, c); workgroup (0, c) also rolls the channel's true-peak history.
 __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.y;
-  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (f >= p.n_frames) return;
   const int C = p.C;
-  const int nh = p.n_l_in[c], nt = p.n_t_in[c];
+  const int nt = p.n_t_in[c];
+  const int64_t F = p.n_frames;
+  if (blockIdx.x == 0) {
+    const int64_t tt = (int64_t)nt + F;
+    const int ktl = (int)min<int64_t>(p.HT, tt);
+    for (int i = threadIdx.x; i < ktl; i += 256) {
+      const int64_t j = tt - ktl + i;
+      p.hist_t_out[(int64_t)c * p.HT + i] = j < nt ? p.hist_t_in[(int64_t)c * p.HT + j] : p.tp[(j - nt) * C + c];
+    }
+    if (threadIdx.x == 0) p.n_t_out[c] = ktl;
+  }
+  const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= F) return;
+  const int nh = p.n_l_in[c];
   const uint32_t T0 = p.t0_in[c];
   const int64_t n = nh + f + 1;  // the sequence known to this frame, local index 0 = absolute T0 - nh
   double sm = 0.0, ss = 0.0;
@@ -244,15 +365,17 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
   }
   sm = wave_sum(sm);
   ss = wave_sum(ss);
-  // integrated window: local [n - wi, n) = absolute [T0 - nh + n - wi, T0 - nh + n)
+  // integrated window: local [n - wi, n) = absolute [lo, hi]
   const int64_t wi = min<int64_t>(p.int_len, n);
-  const int* gp = p.gcount + (int64_t)c * (kUnionCap + 1);
-  const double* gsum = p.gsum + (int64_t)c * (kUnionCap + 1);
+  const int* gp = p.gcount + (int64_t)c * (kSeqCap + 1);
+  const double* gsum = p.gsum + (int64_t)c * (kSeqCap + 1);
   const int ng = gp[n] - gp[n - wi];
   double integ = -100.0, range = 0.0;
   if (ng > 0) {
     integ = (gsum[n] - gsum[n - wi]) / ng;
-    const uint32_t lo = T0 - (uint32_t)nh + (uint32_t)(n - wi), hi = T0 - (uint32_t)nh + (uint32_t)(n - 1);
+    const uint32_t lo = window_lo(T0, nh, f, p.int_len), hi = T0 + (uint32_t)f;
+    const uint32_t clo = window_lo(T0, nh, F - 1, p.int_len), chi = T0;
+    const bool has_core = (int32_t)(chi - clo) >= 0;
     int want[4];
     double gam[2];
     const double qs[2] = {0.10, 0.95};
@@ -264,37 +387,38 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
       want[2 * q + 1] = min(prev + 1, ng - 1);
       gam[q] = vi - floor(vi);
     }
+    // extras in value order, 64 per round; a member's merged rank is (members before it) + rc
+    const MeterExt* ext = p.ext + (int64_t)c * kSeqCap;
+    const int ne = p.n_ext[c];
     float val[4] = {0.f, 0.f, 0.f, 0.f};
-    const unsigned long long* U = p.union_keys + (int64_t)c * kUnionCap;
-    const int g = p.n_union[c];
-    int base = 0;
-    // rows of 64 keys, four rows per step so four LDS/L2 loads are in flight per lane
-    for (int r0 = 0; r0 * 64 < g && base <= want[3]; r0 += 4) {
-      unsigned long long kv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = (r0 + u) * 64 + lane;
-        kv[u] = i < g ? U[i] : ~0ull;
+    int below[4] = {0, 0, 0, 0};  // member extras of merged rank < want
+    bool found[4] = {false, false, false, false};
+    int jb = 0;
+    for (int i0 = 0; i0 < ne; i0 += 64) {
+      const int i = i0 + lane;
+      MeterExt e{0.f, 0u, 0, 0};
+      bool mem = false;
+      if (i < ne) {
+        e = ext[i];
+        mem = (uint32_t)(e.t - lo) <= hi - lo && !(has_core && (uint32_t)(e.t - clo) <= chi - clo);
       }
+      const unsigned long long bm = __ballot(mem);
+      const int rank = jb + __popcll(bm & ((1ull << lane) - 1ull)) + e.rc;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t t = (uint32_t)kv[u];
-        const bool mem = kv[u] != ~0ull && (uint32_t)(t - lo) <= (uint32_t)(hi - lo);
-        const unsigned long long b = __ballot(mem);
-        const int rc = __popcll(b);
-        const int before = __popcll(b & ((1ull << lane) - 1ull));
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const int k = want[w];
-          if (k >= base && k < base + rc) {
-            const unsigned long long hit = __ballot(mem && before == k - base);
-            const int src = __ffsll((long long)hit) - 1;
-            val[w] = unkey((uint32_t)__shfl((int)(uint32_t)(kv[u] >> 32), src, 64));
-          }
+      for (int w = 0; w < 4; ++w) {
+        below[w] += __popcll(__ballot(mem && rank < want[w]));
+        const unsigned long long hit = __ballot(mem && rank == want[w]);
+        if (hit) {
+          found[w] = true;
+          val[w] = __shfl(e.v, __ffsll((long long)hit) - 1, 64);
         }
-        base += rc;
       }
+      jb += __popcll(bm);
     }
+    const float* core = p.core + (int64_t)c * kSeqCap;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      if (!found[w]) val[w] = core[want[w] - below[w]];
     range = lerp_pct(val[2], val[3], gam[1]) - lerp_pct(val[0], val[1], gam[0]);
   }
   const int64_t ntp = nt + f + 1, wt = min<int64_t>(p.peak_len, ntp);
@@ -311,12 +435,20 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
   }
 }
 
-hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s) {
+// prep needs the batch's LUFS_inst only; query also reads its true peaks
+hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s) {
   hipLaunchKernelGGL(meter_prep_kernel, dim3((unsigned)p.C), dim3(1024), 0, s, p);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_meter_query(const MeterPrepParams& p, hipStream_t s) {
   hipLaunchKernelGGL(meter_query_kernel, dim3((unsigned)((p.n_frames + 3) / 4), (unsigned)p.C), dim3(256), 0, s, p);
   return hipGetLastError();
+}
+
+hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s) {
+  const hipError_t e = launch_meter_prep(p, s);
+  return e != hipSuccess ? e : launch_meter_query(p, s);
 }
 
 }  // namespace omega

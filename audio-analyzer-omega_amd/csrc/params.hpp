@@ -9,6 +9,13 @@ constexpr int kMaxRes = 4;
 constexpr int kMaxLog2 = 15;  // twiddle tables for sizes 2^1 .. 2^14 (+1 spare)
 
 // One resolution of the multi-resolution FFT (FFTConfig, multi_resolution_fft.py:26-44).
+// One combine entry. tm = t | op << 24 with op 0: store, 1: add (a later owner of t), 2: store 0
+// (no owner). Entries of a resolution are contiguous; owners of one target run in resolution order.
+struct alignas(16) CombEnt {
+  int tm, j;
+  float c0, c1;
+};
+
 struct ResParam {
   int n;                 // real FFT size N_r
   int offset;            // W - N_r: the resolution reads the last N_r samples of the frame
@@ -26,11 +33,10 @@ struct SpectralParams {
   int64_t n_cf;
   int n_res;
   ResParam res[kMaxRes];
-  // combine plan (multi_resolution_fft.py:353-395): entry e adds cw * interp to target ent_t[e]
-  const int* ent_t;
-  const int* ent_j;
-  const float* ent_frac;
-  const float* wsum;  // [T] weight sum per target (0 -> output 0)
+  // combine plan (multi_resolution_fft.py:353-395): entry e writes or adds
+  // c0 * mag[j] + c1 * mag[j+1] to target t (c0, c1 fold the interpolation fraction, the
+  // psychoacoustic weights of bins j, j+1, the resolution weight and 1 / the target's weight sum)
+  const CombEnt* ent;
   int T;
   float* comb_out;    // [n_cf, T] or nullptr
   // true peak (professional_meters.py:283-299)
@@ -61,10 +67,25 @@ struct KWeightParams {
 };
 
 // Meter aggregates (meters.hip): per-channel double-buffered state (in -> out) plus per-batch scratch.
+// Meter aggregate capacities: frames per launch (the host splits longer batches), history length
+// (>= integrated_len - 1) and the time-ordered sequence history ++ batch.
+constexpr int kMeterChunk = 2048;
+constexpr int kMeterHistCap = 4096;
+constexpr int kMeterSeqCap = kMeterChunk + kMeterHistCap;
+
+// A gated value outside the batch's common window core: value, absolute frame index, and the number
+// of core values below it.
+struct alignas(16) MeterExt {
+  float v;
+  uint32_t t;
+  int rc;
+  int pad;
+};
+
 struct MeterPrepParams {
   const float* lufs;    // [n_frames * C] batch instantaneous LUFS
   const float* tp;      // [n_frames * C]
-  int64_t n_frames;     // <= 4096 per launch
+  int64_t n_frames;     // <= kMeterChunk per launch
   int C;
   const float* hist_l_in;  // [C, HL] last LUFS_inst values, time order
   const float* hist_t_in;  // [C, HT] last TP values
@@ -83,10 +104,13 @@ struct MeterPrepParams {
   int HL, HT;  // integrated_len - 1, peak_len - 1
   int mom_len, short_len, int_len, peak_len;
   float gate;
-  unsigned long long* union_keys;  // [C, 8192] scratch: sorted gated keys of history ++ batch
-  int* n_union;                    // [C]
-  int* gcount;                     // [C, 8193] gated-count prefix in time order
-  double* gsum;                    // [C, 8193] gated-sum prefix in time order
+  // per-batch scratch written by meter_prep_kernel for meter_query_kernel
+  float* core;      // [C, kMeterSeqCap] gated values in every window of the batch, ascending
+  MeterExt* ext;    // [C, kMeterSeqCap] the other gated values of the batch's windows, ascending
+  int* n_core;      // [C]
+  int* n_ext;       // [C]
+  int* gcount;      // [C, kMeterSeqCap + 1] gated-count prefix in time order
+  double* gsum;     // [C, kMeterSeqCap + 1] gated-sum prefix in time order
   double* out;                     // [n_frames * C, 5]
 };
 

@@ -63,10 +63,8 @@ __device__ __forceinline__ void rfft_magnitudes(float2* buf, const float2* __res
 }
 
 // Multi-resolution kernel for one resolution of K = N_r/2 complex points (A3-A5). Launched once per
-// resolution, in resolution order. Combine entries carry a mode (the per-target restatement of
-// multi_resolution_fft.py:387-395):
-//   0: out = v*cw/wsum (sole owner)   1: out = v*cw (first of several owners)
-//   2: out += v*cw (middle owner)     3: out = (out + v*cw)/wsum (last owner)   4: out = 0 (no owner)
+// resolution, in resolution order: a target with several owners (multi_resolution_fft.py:387-395)
+// is stored by its first owner's kernel and accumulated by the later ones (CombEnt).
 template <int K, int NTH = threads_for<K>()>
 __global__ __launch_bounds__(NTH, 2 * NTH / 256) void mrfft_kernel(SpectralParams p, int r) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -78,8 +76,18 @@ __global__ __launch_bounds__(NTH, 2 * NTH / 256) void mrfft_kernel(SpectralParam
   const float* __restrict__ x = p.x + f * p.frame_stride + c * p.chan_stride + rp.offset;
   const float2* x2 = reinterpret_cast<const float2*>(x);
   const float2* w2 = reinterpret_cast<const float2*>(rp.win);
+  // twiddles and this thread's first combine entries are fetched together with the frame: one
+  // global-memory latency before the transform instead of one per pass and per epilogue load
+  using FFT = BlockFFT<K, NTH>;
+  const typename FFT::Tw tw = FFT::load_tw(p.tw[ilog2(K)], tid);
+  constexpr int EP = NTH >= 256 ? 1 : 256 / NTH;
+  CombEnt ent[EP];
+  static_for<0, EP>([&](auto i) {
+    const int e = rp.ent_begin + tid + i * NTH;
+    if (p.comb_out && e < rp.ent_end) ent[i] = p.ent[e];
+  });
   // the first FFT pass reads the windowed frame straight from global memory (coalesced float2)
-  BlockFFT<K, NTH>::run_from(buf, p.tw[ilog2(K)], tid, [&](int i) {
+  FFT::run_from(buf, tw, tid, [&](int i) {
     const float2 a = x2[i], w = w2[i];
     return make_float2(a.x * w.x, a.y * w.y);
   });
@@ -92,32 +100,30 @@ __global__ __launch_bounds__(NTH, 2 * NTH / 256) void mrfft_kernel(SpectralParam
   }
   if (p.comb_out) {
     float* o = p.comb_out + cf * p.T;
-    for (int e = rp.ent_begin + tid; e < rp.ent_end; e += NTH) {
-      const int te = p.ent_t[e];
-      const int t = te & 0xFFFFFF, mode = te >> 24;
-      if (mode == 4) {
-        o[t] = 0.f;
-        continue;
-      }
-      const int j = p.ent_j[e];
-      const float fr = p.ent_frac[e];
-      const float m0 = mag[magidx<K, NTH>(j)] * wgt[j];
-      const float v = (fr != 0.f ? fmaf(fr, mag[magidx<K, NTH>(j + 1)] * wgt[j + 1] - m0, m0) : m0) * rp.cw;
-      if (mode == 0)
-        o[t] = v / p.wsum[t];
-      else if (mode == 1)
+    auto apply = [&](const CombEnt& en) {
+      const int t = en.tm & 0xFFFFFF, op = en.tm >> 24;
+      const float v = fmaf(en.c1, mag[magidx<K, NTH>(en.j + 1)], en.c0 * mag[magidx<K, NTH>(en.j)]);
+      if (op == 0)
         o[t] = v;
-      else if (mode == 2)
+      else if (op == 1)
         o[t] += v;
       else
-        o[t] = (o[t] + v) / p.wsum[t];
-    }
+        o[t] = 0.f;
+    };
+    static_for<0, EP>([&](auto i) {
+      if (rp.ent_begin + tid + i * NTH < rp.ent_end) apply(ent[i]);
+    });
+    for (int e = rp.ent_begin + tid + EP * NTH; e < rp.ent_end; e += NTH) apply(p.ent[e]);
   }
 }
 
+// True-peak workgroup size: 1024 threads (16 waves, 4 per SIMD) for the 8192-point transforms.
+template <int K>
+constexpr int tp_threads() { return K == 8192 ? 1024 : threads_for<K>(); }
+
 // True peak of one frame of M = 2K samples (dBTP; float32 like scipy on float32 input).
-template <int K, int NTH = threads_for<K>()>
-__global__ __launch_bounds__(NTH, 2) void truepeak_kernel(SpectralParams p) {
+template <int K, int NTH = tp_threads<K>()>
+__global__ __launch_bounds__(NTH, (NTH / 256 > 2 ? NTH / 256 : 2)) void truepeak_kernel(SpectralParams p) {
   constexpr int M = 2 * K;
   using FFT = BlockFFT<K, NTH>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -128,7 +134,8 @@ __global__ __launch_bounds__(NTH, 2) void truepeak_kernel(SpectralParams p) {
   const int64_t f = cf / p.C, c = cf % p.C;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride);
   float mx = 0.f;  // p = 0 phase: the samples themselves (every one is loaded exactly once below)
-  FFT::run_from(buf, p.tw[ilog2(K)], tid, [&](int i) {
+  const typename FFT::Tw tw = FFT::load_tw(p.tw[ilog2(K)], tid);  // shared by all four transforms
+  FFT::run_from(buf, tw, tid, [&](int i) {
     const float2 a = x2[i];
     mx = fmaxf(mx, fmaxf(fabsf(a.x), fabsf(a.y)));
     return a;
@@ -157,13 +164,14 @@ __global__ __launch_bounds__(NTH, 2) void truepeak_kernel(SpectralParams p) {
   float fmx = 0.f;
 #pragma unroll 1
   for (int P = 1; P <= 3; ++P) {
-    // opaque per-iteration table pointers: stop LICM from hoisting (and keeping live across the
-    // loop) every twiddle and rotation load of the three inverse transforms
-    // (tid is laundered too: otherwise every LDS address of the inlined FFT, a function of tid
-    // alone, is hoisted out of the loop and pinned in VGPRs)
-    const float2* twK = p.tw[ilog2(K)];
+    // opaque per-iteration values: stop LICM from hoisting (and keeping live across the loop) the
+    // twiddle powers and rotation loads of the three inverse transforms (tid is laundered too:
+    // otherwise every LDS address of the inlined FFT, a function of tid alone, is hoisted out of
+    // the loop and pinned in VGPRs)
     int tl = tid;
-    asm volatile("" : "+s"(twK), "+s"(rot), "+v"(tl));
+    typename FFT::Tw twl = tw;
+    twl.launder();
+    asm volatile("" : "+s"(rot), "+v"(tl));
     __syncthreads();  // the previous readers of buf are done
     const float nyq = P == 2 ? 0.f : (P == 1 ? kS2 : -kS2);  // cos(pi P / 4)
     static_for<0, PB>([&](auto b) {
@@ -195,7 +203,7 @@ __global__ __launch_bounds__(NTH, 2) void truepeak_kernel(SpectralParams p) {
     });
     __syncthreads();
     // the last pass reduces straight from registers: no LDS write of the inverse transform
-    FFT::run_to(buf, twK, tl, [&](int, float2 z) { fmx = fmaxf(fmx, fmaxf(fabsf(z.x), fabsf(z.y))); });
+    FFT::run_to(buf, twl, tl, [&](int, float2 z) { fmx = fmaxf(fmx, fmaxf(fabsf(z.x), fabsf(z.y))); });
   }
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
   if (tid == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
@@ -211,7 +219,7 @@ __global__ __launch_bounds__(NTH, 2 * NTH / 256) void rfft_kernel(RfftParams p) 
   const int64_t i = blockIdx.x;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + i * (2 * K));
   const float2* w2 = reinterpret_cast<const float2*>(p.win);
-  FFT::run_from(buf, p.tw[ilog2(K)], tid, [&](int n) {
+  FFT::run_from(buf, FFT::load_tw(p.tw[ilog2(K)], tid), tid, [&](int n) {
     const float2 a = x2[n], w = w2[n];
     return make_float2(a.x * w.x, a.y * w.y);
   });
@@ -295,7 +303,7 @@ hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
   if (p.tp_out) {
 #define OMEGA_TP(K) \
-  hipLaunchKernelGGL(truepeak_kernel<K>, grid, dim3(threads_for<K>()), K * sizeof(float2) + 16 * sizeof(float), \
+  hipLaunchKernelGGL(truepeak_kernel<K>, grid, dim3(tp_threads<K>()), K * sizeof(float2) + 16 * sizeof(float), \
                      s, p)
     OMEGA_SWITCH_K(W, OMEGA_TP)
 #undef OMEGA_TP

@@ -180,6 +180,26 @@ def test_meter_aggregates_exact_on_injected_values(me):
     np.testing.assert_allclose(dev, ref, rtol=0, atol=1e-9)
 
 
+def test_meter_aggregates_random_batches():
+    """Randomised stream: gated/ungated mixtures, silent stretches (no gated value in the window),
+    repeated values, and batch sizes on both sides of the rank-sort / bitonic switch (1024) and the
+    per-launch chunk (2048); exact against the float64 restatement."""
+    from omega_gpu import Engine, Resolution
+    rng = np.random.default_rng(5)
+    n = 12000
+    li = rng.uniform(-90, -5, n).astype(np.float32)
+    li[3000:7000] = -95.0                        # a silent stretch: the window empties of gated values
+    li[8000:8400] = np.float32(-23.0)            # ties
+    tp = rng.uniform(-40, 0, n).astype(np.float32)
+    e = Engine([Resolution((20, 20000), 512, 256, 1.0)], FS, 20000, 2, frame_size=512)
+    cuts = np.cumsum([1, 17, 256, 1023, 1024, 1025, 2048, 2049, 3000, 5])
+    cuts = [0] + [int(c) for c in cuts if c < n] + [n]
+    dev = np.concatenate([e.meter_update(li[a:b], tp[a:b], b - a) for a, b in zip(cuts[:-1], cuts[1:])])
+    st = R.MeterState(FS)
+    ref = np.array([[v for v in st.update(np.ones(1), float(li[f]), float(tp[f])).values()] for f in range(n)])
+    np.testing.assert_allclose(dev, ref, rtol=0, atol=1e-9)
+
+
 def test_batched_frames_match_facade(me):
     """The fused batch path (process_frames with meters) equals frame-by-frame calculate_lufs."""
     from omega_gpu import Engine, Resolution
