@@ -869,6 +869,17 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
   return 0;
 }
 
+int omega_process_stream(omega_ctx* c, const float* x, int64_t n_samples, int32_t hop, int64_t channel_stride,
+                         const omega_outputs* out, int mem, int64_t* n_frames_out) {
+  if (!c) return OMEGA_EINVAL;
+  if (n_frames_out) *n_frames_out = 0;
+  if (hop < 1 || n_samples < 0) return fail(c, OMEGA_EINVAL, "hop must be >= 1 and n_samples >= 0");
+  const int W = c->cfg.frame_size;
+  const int64_t nf = n_samples < W ? 0 : (n_samples - W) / hop + 1;
+  if (n_frames_out) *n_frames_out = nf;
+  return omega_process_frames(c, x, nf, hop, channel_stride, out, mem);
+}
+
 int omega_combine(omega_ctx* c, const float* const* mags, int64_t n_cf, float* out, int mem) {
   if (!c || !mags || !out) return OMEGA_EINVAL;
   if (n_cf <= 0) return n_cf == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");

@@ -119,9 +119,15 @@ class Engine:
         return np.empty(shape, dtype=dtype)
 
     # -- the fused per-channel-frame path --
+    def process_stream(self, x, n_samples: int, hop: int, channel_stride: int = 0, **kw) -> Dict:
+        """Stream layout (omega_process_stream): one frame per `hop` samples once W samples have
+        arrived; channel c at x[c * channel_stride:]. Same keywords and outputs as process_frames."""
+        n_frames = 0 if n_samples < self.W else (n_samples - self.W) // hop + 1
+        return self.process_frames(x, n_frames, hop, channel_stride, _stream=(n_samples, hop), **kw)
+
     def process_frames(self, x, n_frames: int, frame_stride: int, channel_stride: int, *, combined=True,
                        lufs=True, true_peak=True, meters=False, mags=False, weighted=False,
-                       out: Optional[Dict] = None) -> Dict:
+                       out: Optional[Dict] = None, _stream=None) -> Dict:
         """Run the hot path over n_frames x n_channels channel-frames of x (flat float32, host numpy
         or device torch). Returns a dict of the requested outputs (numpy or torch, like x)."""
         dev = _is_torch(x)
@@ -153,9 +159,15 @@ class Engine:
             outs.mag[r] = _ptr(o.get(f"mag{r}"))
         if dev:
             self._bind_stream(x)
-        self._check(L.lib().omega_process_frames(self._ctx, _ptr(x), int(n_frames), int(frame_stride),
-                                                 int(channel_stride), C.byref(outs),
-                                                 L.MEM_DEVICE if dev else L.MEM_HOST))
+        mem = L.MEM_DEVICE if dev else L.MEM_HOST
+        if _stream is not None:
+            got = C.c_int64(0)
+            self._check(L.lib().omega_process_stream(self._ctx, _ptr(x), int(_stream[0]), int(_stream[1]),
+                                                     int(channel_stride), C.byref(outs), mem, C.byref(got)))
+            assert got.value == n_frames
+        else:
+            self._check(L.lib().omega_process_frames(self._ctx, _ptr(x), int(n_frames), int(frame_stride),
+                                                     int(channel_stride), C.byref(outs), mem))
         return o
 
     def combine(self, mags: Dict[int, np.ndarray], n_cf: int = 1) -> np.ndarray:

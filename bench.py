@@ -38,8 +38,8 @@ BYTES_CF = 4 * W + 4 * (T + 2)                                                  
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -77,6 +77,17 @@ def kernel_time_ms(eng, xd, reps=20):
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / reps, ncf
+
+
+def tp_traffic():
+    """HBM bytes per true-peak launch from the newest committed counter passes (profiles/rNN_tp_traffic.json,
+    written by tools/profile_round.sh + tools/summarize_round.py), or None."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_tp_traffic.json")))
+    if not fs:
+        return None, None
+    d = json.load(open(fs[-1]))
+    return d["traffic_bytes"], os.path.relpath(fs[-1], REPO)
 
 
 def cpu_baseline(seconds):
@@ -125,10 +136,11 @@ def main():
                      "meters": torch.empty(ncf, 5, dtype=torch.float64, device=dev)})
     gather = world > 1 and not a.no_gather
     if gather:
-        import torch.distributed as dist
+        from omega_gpu import dist as D
         # per-frame output vector: combined[512] + lufs + tp + 5 meters (as float32) = 519 floats
-        packs = [torch.empty(ncf, T + 7, device=dev) for _ in range(2)]
-        recv = [[torch.empty(ncf, T + 7, device=dev) for _ in range(world)] if rank == 0 else None for _ in range(2)]
+        packs = [torch.empty(ncf, D.pack_width(T), device=dev) for _ in range(2)]
+        recv = [[torch.empty(ncf, D.pack_width(T), device=dev) for _ in range(world)] if rank == 0 else None
+                for _ in range(2)]
         pending = [None, None]
 
     def step(i):
@@ -137,12 +149,7 @@ def main():
             pending[b].wait()
         o = eng.process_frames(x, FRAMES, C * W, W, meters=True, out=bufs[b])
         if gather:
-            p = packs[b]
-            p[:, :T].copy_(o["combined"])
-            p[:, T].copy_(o["lufs_inst"])
-            p[:, T + 1].copy_(o["true_peak_db"])
-            p[:, T + 2:].copy_(o["meters"])
-            pending[b] = dist.gather(p, recv[b], dst=0, async_op=True)
+            pending[b] = D.gather_to_root(D.pack_outputs(o, T, packs[b]), recv[b], async_op=True)
 
     def barrier():
         if world > 1:
@@ -180,6 +187,7 @@ def main():
     kt_ms, kcf = kernel_time_ms(eng, x)
     flop_launch = FLOP_TP * kcf
     achieved = flop_launch / (kt_ms * 1e-3) / 1e12
+    traffic, traffic_src = tp_traffic()
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
@@ -196,10 +204,15 @@ def main():
                        "parallelism": f"frames sharded over {world} GPU(s)" + (", RCCL gather to rank 0" if gather else "")},
             "roofline": {"bound": "mfma", "kernel": "truepeak_kernel<8192> (4x true peak, fp32)",
                          "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+                         "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "kernel_ms": kt_ms, "flop_per_launch": flop_launch,
-                         "note": "fp32 VALU-bound (fp32 MFMA peak = fp32 vector peak); algorithmic flops per "
-                                 "channel-frame from SURVEY.md §8(d) TP formula"},
+                         "traffic_unit": "bytes per launch (HBM, FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": kcf * (4 * W + 4),
+                         "note": "fp32 VALU/LDS-bound (fp32 MFMA peak = fp32 vector peak); algorithmic flops per "
+                                 "channel-frame from SURVEY.md §8(d) TP formula (the reference's resample "
+                                 "algorithm); kernel_ms = HIP-event average of 20 back-to-back launches on the "
+                                 "launch stream"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

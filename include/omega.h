@@ -11,6 +11,9 @@
  *                          + ProfessionalMetering.calculate_lufs       omega4/panels/professional_meters.py:231-281
  *                          (batched over channel-frames; the reference calls these once per display frame,
  *                           omega4_main.py:707-717 and professional_meters.py:348-351)
+ *   omega_process_stream   the same over the stream layout: frame f = samples [f*hop, f*hop + W) of one
+ *                          buffer per channel (the CircularBuffer.read_latest(N) view of :52-133 once
+ *                          W samples have arrived)
  *   omega_combine          combine_results_optimized                   multi_resolution_fft.py:335-408
  *   omega_true_peak        ProfessionalMetering.calculate_true_peak    professional_meters.py:283-299
  *   omega_k_weighting      ProfessionalMetering.apply_k_weighting      professional_meters.py:129-153
@@ -121,6 +124,12 @@ int omega_synchronize(omega_ctx* ctx);
 /* The fused per-channel-frame hot path over n_frames x n_channels frames of W samples. */
 int omega_process_frames(omega_ctx* ctx, const float* x, int64_t n_frames, int64_t frame_stride,
                          int64_t channel_stride, const omega_outputs* out, int mem);
+
+/* Stream layout: n_samples per channel (channel c at x + c*channel_stride), one frame per hop
+ * samples once a full window has arrived: n_frames = n_samples < W ? 0 : (n_samples - W)/hop + 1,
+ * frame f = x[f*hop, f*hop + W). hop must be even; *n_frames_out (may be NULL) receives the count. */
+int omega_process_stream(omega_ctx* ctx, const float* x, int64_t n_samples, int32_t hop, int64_t channel_stride,
+                         const omega_outputs* out, int mem, int64_t* n_frames_out);
 
 /* combine_results_optimized over externally supplied weighted magnitudes; mags[r] may be NULL
  * (resolution absent from the results dict). out: [n_cf, T]. */

@@ -341,6 +341,13 @@ def test_stream_layout_hop(cfg2):
         comb, _ = R.combine(res, [R.FFTConfig((20, 20000), 4096, 1024, 1.0)], FS, 20000, 256)
         assert normwise(out["combined"][f], comb) < SPEC_TOL
         assert abs(out["true_peak_db"][f] - R.true_peak(fr)) < TP_TOL_DB
+    # omega_process_stream: the same frames from (n_samples, hop); a partial trailing hop is dropped
+    eng2 = Engine([Resolution((20, 20000), 4096, 1024, 1.0)], FS, 20000, 256)
+    st = eng2.process_stream(s, len(s) - 7, H, combined=True, true_peak=True)
+    assert st["combined"].shape == (F - 1, 256)
+    np.testing.assert_array_equal(st["combined"], out["combined"][:F - 1])
+    np.testing.assert_array_equal(st["true_peak_db"], out["true_peak_db"][:F - 1])
+    assert eng2.process_stream(s, W - 1, H)["combined"].shape == (0, 256)
 
 
 def test_zero_frames_is_noop():

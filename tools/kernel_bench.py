@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one stage of the cfg2 hot path in isolation (for rocprofv3 counter passes and A/B timing).
 
-  python tools/kernel_bench.py {tp,kw,mrfft,meters,all} [--reps N]
+  python tools/kernel_bench.py {tp,kw,mrfft,meters,all,host} [--reps N]
 """
 import argparse
 import os
@@ -33,7 +33,12 @@ def main():
     comb = torch.empty(ncf, 512, device="cuda")
     met = torch.empty(ncf, 5, dtype=torch.float64, device="cuda")
 
+    xh = bench.cfg2_input()
+    host_out = {}
+
     def run():
+        if a.stage == "host":  # host buffers in and out: PCIe-inclusive rate of the full path
+            host_out.update(eng.process_frames(xh, 256, 2 * 16384, 16384, meters=True))
         if a.stage in ("tp", "all"):
             eng._check(lib.omega_true_peak(eng._ctx, x.data_ptr(), ncf, 16384, out["tp"].data_ptr(), L.MEM_DEVICE))
         if a.stage in ("kw", "all"):
@@ -53,7 +58,9 @@ def main():
         run()
     e.record()
     torch.cuda.synchronize()
-    print(f"{a.stage}: {s.elapsed_time(e) / a.reps * 1e3:.1f} us per call")
+    us = s.elapsed_time(e) / a.reps * 1e3
+    print(f"{a.stage}: {us:.1f} us per call" + (f" = {ncf / us * 1e6:.0f} channel-frames/s (host in/out)"
+                                                  if a.stage == "host" else ""))
 
 
 if __name__ == "__main__":

@@ -11,7 +11,7 @@ if [[ $STEPS == *tests* ]]; then
   tail -2 gpurun_out/tests.log
 fi
 if [[ $STEPS == *stages* ]]; then
-  for st in tp kw mrfft meters all; do timeout -k 10 120 python tools/kernel_bench.py $st --reps 50; done
+  for st in tp kw mrfft meters all host; do timeout -k 10 120 python tools/kernel_bench.py $st --reps 50; done
 fi
 if [[ $STEPS == *bench* ]]; then
   timeout -k 10 300 python bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/bench.json
