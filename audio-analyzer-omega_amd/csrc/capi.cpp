@@ -272,7 +272,7 @@ int get_kw_tab(omega_ctx* c, int M, BiquadTab** out) {
     return 0;
   }
   const double fs = c->cfg.sample_rate;
-  const int L = M / 256;
+  const int L = kw_chunk(M);
   std::vector<BiquadTab> t = {make_biquad_tab(butter2_highpass(38.0, fs), L),
                               make_biquad_tab(butter2_highpass(1500.0, fs), L)};
   BiquadTab* d = nullptr;

@@ -164,15 +164,16 @@ __device__ __forceinline__ void fft_pass(float2 w1, int tid, Load&& load, Store&
 // Radix plan R0, R1, ... applied in order with NS = product of the radices before each pass; I is
 // the pass index. FIRST/LAST: whether the first pass loads through `first` (e.g. straight from
 // global memory) and the last pass stores through `last` (e.g. a register-side reduction) instead
-// of the LDS buffer.
+// of LDS. PP (ping-pong): each pass reads `buf` and writes `alt`, then the two swap -- one barrier per
+// pass instead of two (an in-place pass needs a barrier between all reads and all writes).
 template <int K, int NTH, int I, int NS, int PNS, int PR, int... Rs>
 struct StockhamChain;
 template <int K, int NTH, int I, int NS, int PNS, int PR>
 struct StockhamChain<K, NTH, I, NS, PNS, PR> {
   template <class TW>
   static __device__ __forceinline__ void load_tw(const float2*, int, TW&) {}
-  template <bool FIRST, bool LAST, class TW, class F, class G>
-  static __device__ __forceinline__ void run(float2*, const TW&, int, F&&, G&&) {}
+  template <bool FIRST, bool LAST, bool PP, class TW, class F, class G>
+  static __device__ __forceinline__ void run(float2*, float2*, const TW&, int, F&&, G&&) {}
   static __device__ __forceinline__ int out(int i) { return swz<PNS, PR>(i); }
 };
 template <int K, int NTH, int I, int NS, int PNS, int PR, int R, int... Rs>
@@ -187,14 +188,16 @@ struct StockhamChain<K, NTH, I, NS, PNS, PR, R, Rs...> {
     }
     Next::load_tw(tw, t, w);
   }
-  template <bool FIRST, bool LAST, class TW, class F, class G>
-  static __device__ __forceinline__ void run(float2* buf, const TW& w, int t, F&& first, G&& last) {
+  template <bool FIRST, bool LAST, bool PP, class TW, class F, class G>
+  static __device__ __forceinline__ void run(float2* buf, float2* alt, const TW& w, int t, F&& first, G&& last) {
+    float2* dst = PP ? alt : buf;
     auto lds_load = [&](int i) { return buf[swz<PNS, PR>(i)]; };
-    auto lds_store = [&](int i, float2 v) { buf[swz<NS, R>(i)] = v; };
+    auto lds_store = [&](int i, float2 v) { dst[swz<NS, R>(i)] = v; };
     constexpr bool in_global = FIRST && NS == 1;
     constexpr bool out_regs = LAST && kLastPass;
-    // in place in LDS needs the mid-pass barrier; a global-source or register-sink pass does not
-    constexpr bool sync_mid = !in_global && !out_regs;
+    // in place in LDS needs the mid-pass barrier; a global-source, register-sink or ping-pong pass
+    // does not
+    constexpr bool sync_mid = !in_global && !out_regs && !PP;
     if constexpr (in_global && out_regs)
       fft_pass<K, R, NS, NTH, false>(w.w[I], t, first, last);
     else if constexpr (in_global)
@@ -204,21 +207,23 @@ struct StockhamChain<K, NTH, I, NS, PNS, PR, R, Rs...> {
     else
       fft_pass<K, R, NS, NTH, sync_mid>(w.w[I], t, lds_load, lds_store);
     if constexpr (!out_regs) __syncthreads();  // results visible to the next pass / the caller
-    Next::template run<FIRST, LAST>(buf, w, t, first, last);
+    Next::template run<FIRST, LAST, PP>(dst, PP ? buf : alt, w, t, first, last);
   }
   static __device__ __forceinline__ int out(int i) { return Next::out(i); }
 };
 
 // Forward complex FFT of K points with NTH threads. Natural order in (identity swizzle) and out
-// (element i at buf[out(i)]). Twiddles: Tw from load_tw(tw) with tw = exp(-2 pi i m / K), m < K.
-// run(): input already in LDS and the caller synchronised; run_from(first): the first pass reads
-// logical element i as first(i) (no LDS write of the input; the caller must make sure no one still
-// reads buf); run_to(last): the last pass hands outputs to last(i, v) instead of LDS (the caller
-// synchronises before reusing buf).
+// (element i at out(i) of the result buffer). Twiddles: Tw from load_tw(tw) with
+// tw = exp(-2 pi i m / K), m < K. run(): input already in LDS (`buf`) and the caller synchronised;
+// run_from(first): the first pass reads logical element i as first(i) (no LDS write of the input;
+// the caller must make sure no one still reads the buffers written); run_to(last): the last pass
+// hands outputs to last(i, v) instead of LDS (the caller synchronises before reusing the buffers).
+// The *_pp forms ping-pong between buf and alt; result(buf, alt) names the buffer holding the output.
 template <int K, int NTH, int... Rs>
 struct FFTPlan {
   using Chain = StockhamChain<K, NTH, 0, 1, 0, 1, Rs...>;
   using Tw = TwReg<sizeof...(Rs)>;
+  static constexpr int kPasses = sizeof...(Rs);
   static __device__ __forceinline__ Tw load_tw(const float2* __restrict__ tw, int t) {
     Tw w;
     Chain::load_tw(tw, t, w);
@@ -227,17 +232,31 @@ struct FFTPlan {
   static __device__ __forceinline__ void run(float2* b, const Tw& w, int t) {
     auto none = [](int) { return make_float2(0.f, 0.f); };
     auto sink = [](int, float2) {};
-    Chain::template run<false, false>(b, w, t, none, sink);
+    Chain::template run<false, false, false>(b, b, w, t, none, sink);
   }
   template <class F>
   static __device__ __forceinline__ void run_from(float2* b, const Tw& w, int t, F&& first) {
     auto sink = [](int, float2) {};
-    Chain::template run<true, false>(b, w, t, first, sink);
+    Chain::template run<true, false, false>(b, b, w, t, first, sink);
   }
   template <class G>
   static __device__ __forceinline__ void run_to(float2* b, const Tw& w, int t, G&& last) {
     auto none = [](int) { return make_float2(0.f, 0.f); };
-    Chain::template run<false, true>(b, w, t, none, last);
+    Chain::template run<false, true, false>(b, b, w, t, none, last);
+  }
+  // ping-pong forms. run_from_pp: every pass writes LDS, the first into alt; returns the buffer
+  // holding the result. run_to_pp: input in b; passes alternate b -> alt -> b ...; the last pass
+  // reads LDS and hands its outputs to `last`.
+  template <class F>
+  static __device__ __forceinline__ float2* run_from_pp(float2* b, float2* alt, const Tw& w, int t, F&& first) {
+    auto sink = [](int, float2) {};
+    Chain::template run<true, false, true>(b, alt, w, t, first, sink);  // pass 1 writes alt, pass 2 b, ...
+    return kPasses % 2 ? alt : b;
+  }
+  template <class G>
+  static __device__ __forceinline__ void run_to_pp(float2* b, float2* alt, const Tw& w, int t, G&& last) {
+    auto none = [](int) { return make_float2(0.f, 0.f); };
+    Chain::template run<false, true, true>(b, alt, w, t, none, last);
   }
   static __device__ __forceinline__ int out(int i) { return Chain::out(i); }
 };
@@ -261,6 +280,31 @@ template <int NTH> struct BlockFFTPlan<256, NTH> { using type = FFTPlan<256, NTH
 
 template <int K, int NTH = threads_for<K>()>
 using BlockFFT = typename BlockFFTPlan<K, NTH>::type;
+
+// ---- cross-lane moves without address registers (DPP / ds_swizzle / readlane) ----
+// lane l reads lane ((l & AND) | OR) ^ XOR of its 32-lane half (ds_swizzle bitmask mode)
+template <int AND, int OR, int XOR>
+__device__ __forceinline__ float swizzle32(float v) {
+  static_assert(AND < 32 && OR < 32 && XOR < 32, "5-bit masks");
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), AND | (OR << 5) | (XOR << 10)));
+}
+// whole-wave shift by one lane: SHR reads lane l-1 (lane 0 reads 0), otherwise lane l+1 (lane 63 reads 0)
+template <bool SHR>
+__device__ __forceinline__ float wave_shift1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), SHR ? 0x138 : 0x130, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float read_lane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+// sum over the wave, result in every lane (xor swizzles within halves, then the two half sums)
+__device__ __forceinline__ float wave_sum_sw(float v) {
+  v += swizzle32<31, 0, 1>(v);
+  v += swizzle32<31, 0, 2>(v);
+  v += swizzle32<31, 0, 4>(v);
+  v += swizzle32<31, 0, 8>(v);
+  v += swizzle32<31, 0, 16>(v);
+  return read_lane(v, 0) + read_lane(v, 32);
+}
 
 // ---- block reductions ----
 __device__ __forceinline__ float wave_max(float v) {
@@ -289,6 +333,18 @@ __device__ __forceinline__ float block_max(float v, float* red, int tid) {
   float r = red[0];
 #pragma unroll
   for (int w = 1; w < NTH / 64; ++w) r = fmaxf(r, red[w]);
+  return r;
+}
+// block sum of float partials accumulated in double across waves (result in every thread)
+template <int NTH = NT>
+__device__ __forceinline__ double block_sum_f(float v, double* red, int tid) {
+  const float w = wave_sum_sw(v);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = (double)w;
+  __syncthreads();
+  double r = red[0];
+#pragma unroll
+  for (int i = 1; i < NTH / 64; ++i) r += red[i];
   return r;
 }
 template <int NTH = NT>

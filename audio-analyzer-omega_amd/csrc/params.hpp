@@ -54,6 +54,11 @@ struct BiquadTab {
   float pw[64][4];     // P^(l+1), P = A^L, row-major 2x2
 };
 
+// K-weighting workgroup: up to 32 samples per thread (M/32 threads, 64..512), the chunk length L of
+// the scan tables (make_biquad_tab) follows from it.
+constexpr int kw_threads(int M) { return M / 32 < 64 ? 64 : (M / 32 > 512 ? 512 : M / 32); }
+constexpr int kw_chunk(int M) { return M / kw_threads(M); }
+
 struct KWeightParams {
   const float* x;
   int64_t frame_stride, chan_stride;

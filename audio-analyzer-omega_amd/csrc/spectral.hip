@@ -121,21 +121,23 @@ __global__ __launch_bounds__(NTH, 2 * NTH / 256) void mrfft_kernel(SpectralParam
 template <int K>
 constexpr int tp_threads() { return K == 8192 ? 1024 : threads_for<K>(); }
 
-// True peak of one frame of M = 2K samples (dBTP; float32 like scipy on float32 input).
+// True peak of one frame of M = 2K samples (dBTP; float32 like scipy on float32 input). The four
+// transforms ping-pong between two K-point LDS buffers (one barrier per pass).
 template <int K, int NTH = tp_threads<K>()>
 __global__ __launch_bounds__(NTH, (NTH / 256 > 2 ? NTH / 256 : 2)) void truepeak_kernel(SpectralParams p) {
   constexpr int M = 2 * K;
   using FFT = BlockFFT<K, NTH>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float2* buf = reinterpret_cast<float2*>(smem);
-  float* red = reinterpret_cast<float*>(smem + K * sizeof(float2));
+  float2* bufA = reinterpret_cast<float2*>(smem);
+  float2* bufB = bufA + K;
+  float* red = reinterpret_cast<float*>(smem + 2 * K * sizeof(float2));
   const int tid = threadIdx.x;
   const int64_t cf = blockIdx.x;
   const int64_t f = cf / p.C, c = cf % p.C;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride);
   float mx = 0.f;  // p = 0 phase: the samples themselves (every one is loaded exactly once below)
   const typename FFT::Tw tw = FFT::load_tw(p.tw[ilog2(K)], tid);  // shared by all four transforms
-  FFT::run_from(buf, tw, tid, [&](int i) {
+  const float2* buf = FFT::run_from_pp(bufA, bufB, tw, tid, [&](int i) {
     const float2 a = x2[i];
     mx = fmaxf(mx, fmaxf(fabsf(a.x), fabsf(a.y)));
     return a;
@@ -162,6 +164,10 @@ __global__ __launch_bounds__(NTH, (NTH / 256 > 2 ? NTH / 256 : 2)) void truepeak
   const float2* rot = p.rot;  // e^{2 pi i k / 4M}, k <= K
   constexpr float kS2 = 7.071067812e-01f;
   float fmx = 0.f;
+  // transform P writes its input into `zin` and runs zin -> zalt -> zin ...; the next transform's
+  // input goes to the buffer the previous one's last pass did not read
+  constexpr bool kOddPasses = FFT::kPasses % 2 == 1;
+  int zsel = buf == bufA ? 1 : 0;  // input buffer of the next transform: not the one the untangle reads
 #pragma unroll 1
   for (int P = 1; P <= 3; ++P) {
     // opaque per-iteration values: stop LICM from hoisting (and keeping live across the loop) the
@@ -171,13 +177,16 @@ __global__ __launch_bounds__(NTH, (NTH / 256 > 2 ? NTH / 256 : 2)) void truepeak
     int tl = tid;
     typename FFT::Tw twl = tw;
     twl.launder();
-    asm volatile("" : "+s"(rot), "+v"(tl));
-    __syncthreads();  // the previous readers of buf are done
+    int roff = 0;  // laundered as an offset, so the loads stay global (a laundered pointer goes flat)
+    asm volatile("" : "+s"(roff), "+v"(tl));
+    const float2* __restrict__ rotl = rot + roff;
+    float2* zin = zsel ? bufB : bufA;
+    float2* zalt = zsel ? bufA : bufB;
     const float nyq = P == 2 ? 0.f : (P == 1 ? kS2 : -kS2);  // cos(pi P / 4)
     static_for<0, PB>([&](auto b) {
       const int k = tl + b * NTH;
       if (NP % NTH == 0 || k < NP) {
-        const float2 r1 = rot[k];
+        const float2 r1 = rotl[k];
         const float2 r2 = cmul(r1, r1);
         const float2 rp = P == 1 ? r1 : (P == 2 ? r2 : cmul(r2, r1));
         const float2 e = cmul(r2, r2);  // e^{2 pi i k / M}
@@ -190,20 +199,22 @@ __global__ __launch_bounds__(NTH, (NTH / 256 > 2 ? NTH / 256 : 2)) void truepeak
         // O = (Y_k - conj Y_{K-k})/2 e. Stored conjugated: a forward FFT then gives conj(ifft).
         const float2 E = make_float2(0.5f * (yk.x + ykk.x), 0.5f * (yk.y - ykk.y));
         const float2 O = cmul(make_float2(0.5f * (yk.x - ykk.x), 0.5f * (yk.y + ykk.y)), e);
-        buf[k] = make_float2(E.x - O.y, -(E.y + O.x));
+        zin[k] = make_float2(E.x - O.y, -(E.y + O.x));
         if (k != 0) {
-          buf[K - k] = make_float2(E.x + O.y, E.y - O.x);
+          zin[K - k] = make_float2(E.x + O.y, E.y - O.x);
         } else {
           // k = K/2: Z'[K/2] = conj(Y[K/2]), Y[K/2] = X[K/2] rot^P(K/2); stored conjugated = Y
-          const float2 rh = rot[K / 2];
+          const float2 rh = rotl[K / 2];
           const float2 rh2 = cmul(rh, rh);
-          buf[K / 2] = cmul(Xmid, P == 1 ? rh : (P == 2 ? rh2 : cmul(rh2, rh)));
+          zin[K / 2] = cmul(Xmid, P == 1 ? rh : (P == 2 ? rh2 : cmul(rh2, rh)));
         }
       }
     });
     __syncthreads();
     // the last pass reduces straight from registers: no LDS write of the inverse transform
-    FFT::run_to(buf, twl, tl, [&](int, float2 z) { fmx = fmaxf(fmx, fmaxf(fabsf(z.x), fabsf(z.y))); });
+    FFT::run_to_pp(zin, zalt, twl, tl, [&](int, float2 z) { fmx = fmaxf(fmx, fmaxf(fabsf(z.x), fabsf(z.y))); });
+    // the last pass read zin (odd pass count: passes read zin, zalt, zin, ...) -> next input in zalt
+    if (kOddPasses) zsel ^= 1;
   }
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
   if (tid == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
@@ -303,7 +314,9 @@ hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
   if (p.tp_out) {
 #define OMEGA_TP(K) \
-  hipLaunchKernelGGL(truepeak_kernel<K>, grid, dim3(tp_threads<K>()), K * sizeof(float2) + 16 * sizeof(float), \
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&truepeak_kernel<K>), \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 2 * K * sizeof(float2) + 16 * sizeof(float)); \
+  hipLaunchKernelGGL(truepeak_kernel<K>, grid, dim3(tp_threads<K>()), 2 * K * sizeof(float2) + 16 * sizeof(float), \
                      s, p)
     OMEGA_SWITCH_K(W, OMEGA_TP)
 #undef OMEGA_TP

@@ -8,6 +8,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libomega.so")
+if os.environ.get("OMEGA_STAMPS_BUILD") == "1":  # kernel-development build (make stamps), tools/stamps.py
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libomega_stamps.so")
 
 MAX_RES = 4
 N_METERS = 5

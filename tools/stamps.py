@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Phase timings from the timestamp build (make -C audio-analyzer-omega_amd stamps):
+OMEGA_STAMPS_BUILD=1 python tools/stamps.py kw  -- runs the stage on the cfg2 batch and prints, for
+workgroups 0..3, each wave's s_memtime stamps relative to the workgroup's first stamp (in units of
+the shader clock)."""
+import ctypes as C
+import os
+import sys
+
+os.environ["OMEGA_STAMPS_BUILD"] = "1"
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "audio-analyzer-omega_amd"))
+sys.path.insert(0, REPO)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main(stage):
+    import bench
+    from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
+    from omega_gpu import _lib as L
+    x = torch.from_numpy(bench.cfg2_input()).cuda()
+    eng = Engine(NORTHSTAR_RESOLUTIONS, 48000, 20000, target_bins=512, n_channels=2)
+    lib = L.lib()
+    eng._bind_stream(x)
+    li = torch.empty(512, device="cuda")
+    getter = {"kw": "omega_debug_kw_stamps"}[stage]
+    for _ in range(3):
+        eng._check(lib.omega_k_weighting(eng._ctx, x.data_ptr(), 512, 16384, None, li.data_ptr(), L.MEM_DEVICE))
+    torch.cuda.synchronize()
+    buf = np.zeros(4 * 16 * 32, np.uint64)
+    fn = getattr(lib, getter)
+    fn.argtypes = [C.c_void_p]
+    assert fn(buf.ctypes.data) == 0
+    st = buf.reshape(4, 16, 32).astype(np.int64)
+    for b in range(4):
+        base = st[b][st[b] > 0].min() if (st[b] > 0).any() else 0
+        print(f"workgroup {b}")
+        for w in range(16):
+            row = st[b, w]
+            if not (row > 0).any():
+                continue
+            print(f"  w{w:2d} " + " ".join(f"{s}:{int(v - base)}" for s, v in enumerate(row) if v > 0))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "kw")
