@@ -25,9 +25,11 @@ namespace omega {
 hipError_t launch_spectral(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_mrfft(const SpectralParams& p, hipStream_t s);
 hipError_t launch_mrfft_range(const SpectralParams& p, int r0, int r1, hipStream_t s);
+hipError_t launch_mrfft_independent(const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
+hipError_t launch_frame(const SpectralParams& sp, const KWeightParams& kp, hipStream_t s);
 hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_query(const MeterPrepParams& p, hipStream_t s);
@@ -169,7 +171,11 @@ struct omega_ctx {
   float* d_wgt[kMaxRes] = {};
   CombEnt* d_ent = nullptr;
   int ent_begin[kMaxRes] = {}, ent_end[kMaxRes] = {};
-  std::map<int, BiquadTab*> kw_tabs;  // M -> device {hp, shelf}
+  std::map<std::pair<int, int>, BiquadTab*> kw_tabs;  // (M, chunk) -> device {hp, shelf}
+  float4* d_tpx = nullptr;  // true-peak spectrum scratch (16384-sample frames), tpx_cap channel-frames
+  int64_t tpx_cap = 0;
+  bool tp_l2 = false;       // 512-thread true peak with the spectrum in L2 (OMEGA_TP_L2=1; measured slower)
+  bool fuse_frame = false;  // W = 16384: K-weighting + true peak in one kernel (OMEGA_FUSE=1 enables)
   std::map<std::pair<int, int>, float*> windows;  // (m, kind) -> device window
   std::map<int, float2*> rots;                     // m -> true-peak rotation table
   // combine plan as per-target owner lists (CSR) for omega_combine over a subset of resolutions
@@ -265,23 +271,24 @@ int build_twiddles(omega_ctx* c) {
   return 0;
 }
 
-int get_kw_tab(omega_ctx* c, int M, BiquadTab** out) {
-  auto it = c->kw_tabs.find(M);
+int get_kw_tab(omega_ctx* c, int M, int L, BiquadTab** out) {
+  const auto key = std::make_pair(M, L);
+  auto it = c->kw_tabs.find(key);
   if (it != c->kw_tabs.end()) {
     *out = it->second;
     return 0;
   }
   const double fs = c->cfg.sample_rate;
-  const int L = kw_chunk(M);
   std::vector<BiquadTab> t = {make_biquad_tab(butter2_highpass(38.0, fs), L),
                               make_biquad_tab(butter2_highpass(1500.0, fs), L)};
   BiquadTab* d = nullptr;
   int r = upload(c, &d, t);
   if (r) return r;
-  c->kw_tabs[M] = d;
+  c->kw_tabs[key] = d;
   *out = d;
   return 0;
 }
+int get_kw_tab(omega_ctx* c, int M, BiquadTab** out) { return get_kw_tab(c, M, kw_chunk(M), out); }
 
 int get_window(omega_ctx* c, int m, int kind, float** out) {
   auto key = std::make_pair(m, kind);
@@ -345,6 +352,36 @@ int validate(omega_ctx* c, const omega_config* cfg) {
     return fail(c, OMEGA_EUNSUP, "integrated_len %d: 1..4096 supported", cfg->integrated_len);
   if (cfg->momentary_len < 1 || cfg->short_len < 1 || cfg->peak_len < 1)
     return fail(c, OMEGA_EINVAL, "deque lengths must be >= 1");
+  return 0;
+}
+
+void drop_graphs(omega_ctx* c) {
+  for (auto& g : c->graphs) {
+    (void)hipGraphExecDestroy(g.exec);
+    (void)hipGraphDestroy(g.graph);
+  }
+  c->graphs.clear();
+}
+
+// Spectrum scratch of the 512-thread true-peak kernel (W = 16384): 64 KiB per channel-frame, grown
+// on demand up to 8192 channel-frames (larger calls use the register-resident kernel). Growing
+// drops the captured graphs, which hold the old pointer.
+int tp_scratch(omega_ctx* c, int W, int64_t n_cf, float4** out) {
+  *out = nullptr;
+  if (W != 16384 || !c->tp_l2 || n_cf > 8192) return 0;
+  if (n_cf > c->tpx_cap) {
+    const int64_t cap = std::max<int64_t>(n_cf, 512);
+    if (c->d_tpx) {
+      HIPC(c, hipDeviceSynchronize());
+      (void)hipFree(c->d_tpx);
+      c->d_tpx = nullptr;
+      c->tpx_cap = 0;
+    }
+    drop_graphs(c);
+    HIPC(c, hipMalloc(&c->d_tpx, (size_t)cap * (W / 4) * sizeof(float4)));
+    c->tpx_cap = cap;
+  }
+  *out = c->d_tpx;
   return 0;
 }
 
@@ -612,18 +649,35 @@ int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_f
 // fork[0] from the start; K-weighting and then the meter aggregates' prep kernel (it needs the batch's
 // LUFS_inst only) on `s`, whose query kernel then waits for the true peaks; both branches join back
 // into `s`.
-int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, int64_t n_frames,
-                   const float* lufs, const float* tp, double* meters, hipStream_t s) {
+// kp16: the K-weighting parameters with 16-sample-chunk tables for the fused frame kernel (hp null
+// when not built).
+int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, const KWeightParams& kp16, int W,
+                   int64_t n_frames, const float* lufs, const float* tp, double* meters, hipStream_t s) {
   const bool do_tp = sp.tp_out != nullptr, do_kw = kp.lufs_out || kp.weighted_out;
   const bool do_res = sp.comb_out != nullptr || sp.res[0].mag_out || sp.res[1].mag_out || sp.res[2].mag_out ||
                       sp.res[3].mag_out;
   if (!c->concurrent) {
-    if (do_res) HIPC(c, launch_mrfft(sp, s));
+    if (do_res) HIPC(c, c->res_independent ? launch_mrfft_independent(sp, s) : launch_mrfft(sp, s));
     if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
     if (do_kw) HIPC(c, launch_kweight(W, kp, s));
     return meters ? meters_enqueue(c, lufs, tp, n_frames, meters, s, nullptr) : 0;
   }
   HIPC(c, hipEventRecord(c->ev_fork, s));
+  if (W == 16384 && do_tp && do_kw && kp16.hp && c->fuse_frame) {
+    // fused layout: true peak + K-weighting in one kernel on `s`, then the meters; resolutions on fork[0]
+    if (do_res) {
+      HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
+      HIPC(c, c->res_independent ? launch_mrfft_independent(sp, c->fork[0]) : launch_mrfft(sp, c->fork[0]));
+      HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
+    }
+    HIPC(c, launch_frame(sp, kp16, s));
+    if (meters) {
+      const int e = meters_enqueue(c, lufs, tp, n_frames, meters, s, nullptr);
+      if (e) return e;
+    }
+    if (do_res) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
+    return 0;
+  }
   if (do_tp) {
     HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_fork, 0));
     HIPC(c, launch_truepeak(W, sp, c->fork[1]));
@@ -631,7 +685,7 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
   }
   if (do_res) {
     HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
-    HIPC(c, launch_mrfft(sp, c->fork[0]));
+    HIPC(c, c->res_independent ? launch_mrfft_independent(sp, c->fork[0]) : launch_mrfft(sp, c->fork[0]));
     HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
   }
   if (do_kw) HIPC(c, launch_kweight(W, kp, s));
@@ -691,6 +745,8 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
     return fail(c, OMEGA_EHIP, "device %d: %s", device, hipGetErrorString(he));
   }
   c->stream = c->own;
+  if (const char* fz = std::getenv("OMEGA_FUSE")) c->fuse_frame = std::atoi(fz) != 0;
+  if (const char* tl = std::getenv("OMEGA_TP_L2")) c->tp_l2 = std::atoi(tl) != 0;
   if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
     const int v = std::atoi(lay);
     c->concurrent = v != 0;
@@ -721,10 +777,8 @@ void omega_destroy(omega_ctx* c) {
   for (auto& kv : c->chroma_mats) (void)hipFree(kv.second.first);
   for (DevBuf& b : c->stage)
     if (b.p) (void)hipFree(b.p);
-  for (auto& g : c->graphs) {
-    (void)hipGraphExecDestroy(g.exec);
-    (void)hipGraphDestroy(g.graph);
-  }
+  drop_graphs(c);
+  if (c->d_tpx) (void)hipFree(c->d_tpx);
   for (hipStream_t st : {c->cap, c->fork[0], c->fork[1]})
     if (st) (void)hipStreamDestroy(st);
   for (hipEvent_t ev : {c->ev_fork, c->ev_join[0], c->ev_join[1], c->ev_kw})
@@ -745,11 +799,7 @@ int omega_set_graphs(omega_ctx* c, int enable) {
   if (!c) return OMEGA_EINVAL;
   c->use_graph = (enable & 1) != 0;
   c->concurrent = (enable & 2) == 0;
-  for (auto& g : c->graphs) {
-    (void)hipGraphExecDestroy(g.exec);
-    (void)hipGraphDestroy(g.graph);
-  }
-  c->graphs.clear();
+  drop_graphs(c);
   return 0;
 }
 
@@ -787,6 +837,10 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
   sp.frame_stride = frame_stride;
   sp.chan_stride = channel_stride;
   sp.n_cf = ncf;
+  if (out->true_peak_db) {
+    const int e0 = tp_scratch(c, W, ncf, &sp.tp_scratch);
+    if (e0) return e0;
+  }
   std::vector<HostOut> outs;
   const float* dx = x;
   float* tp = out->true_peak_db;
@@ -830,6 +884,15 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
     if (e) return e;
   }
   KWeightParams kp{dx, frame_stride, channel_stride, C, ncf, tabs, tabs ? tabs + 1 : nullptr, lufs, weighted, 0};
+  KWeightParams kp16 = kp;
+  kp16.hp = kp16.shelf = nullptr;
+  if (tabs && W == 16384 && tp && c->fuse_frame) {
+    BiquadTab* t16 = nullptr;
+    e = get_kw_tab(c, W, kFrameChunk, &t16);
+    if (e) return e;
+    kp16.hp = t16;
+    kp16.shelf = t16 + 1;
+  }
   if (mem == OMEGA_MEM_DEVICE && c->use_graph) {
     // replay a captured graph of this exact call (pointers, sizes, meter-state parity), capturing it on
     // first use: removes the per-launch host cost and runs the three branches concurrently
@@ -850,7 +913,7 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
       }
       const int cur0 = c->cur;
       HIPC(c, hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
-      e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->cap);
+      e = enqueue_frames(c, sp, kp, kp16, W, n_frames, lufs, tp, meters, c->cap);
       hipGraph_t graph = nullptr;
       const hipError_t ce = hipStreamEndCapture(c->cap, &graph);
       if (e) return e;
@@ -863,7 +926,7 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
     if (meters) c->cur ^= (int)(((n_frames + kChunkFrames - 1) / kChunkFrames) & 1);
     return 0;
   }
-  e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->stream);
+  e = enqueue_frames(c, sp, kp, kp16, W, n_frames, lufs, tp, meters, c->stream);
   if (e) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
@@ -943,6 +1006,7 @@ int omega_true_peak(omega_ctx* c, const float* x, int64_t n, int32_t m, float* o
   sp.tp_out = dout;
   float2* rot = nullptr;
   e = get_rot(c, m, &rot);
+  if (!e) e = tp_scratch(c, m, n, &sp.tp_scratch);
   if (e) return e;
   sp.rot = rot;
   HIPC(c, launch_spectral(m, sp, c->stream));

@@ -24,8 +24,11 @@
 //     extra or core[k - #extras ranked below k] -- a pass over the extras, no per-frame sort.
 #include "fft.hpp"
 #include "params.hpp"
+#include "stamps.hpp"
 
 namespace omega {
+
+OMEGA_STAMPS_DECL
 
 constexpr int kNewCap = kMeterChunk;
 constexpr int kHistCap = kMeterHistCap;
@@ -132,6 +135,7 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   const int L = nh + F;
   const int64_t thr = (int64_t)T0 + F - p.HL;  // oldest absolute index the next batch's windows reach
   const float gate = p.gate;
+  OMEGA_STAMP(0);
   // 1) stage the sequence and the sorted history (loads of a thread issued together)
 #pragma unroll
   for (int q = 0; q < kSeqCap / 1024; ++q) {
@@ -144,6 +148,7 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     if (i < ns) A[i] = p.skeys_in[(int64_t)c * p.HL + i];
   }
   __syncthreads();
+  OMEGA_STAMP(1);
   auto bkey = [&](int f) -> unsigned long long {
     const float v = V[nh + f];
     return v > gate ? ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)f) : ~0ull;
@@ -191,6 +196,7 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     int dummy;
     Gn = block_excl_scan(gn_part, wsa, tid, dummy);
   }
+  OMEGA_STAMP(2);
   // 3) kept flags (absolute index >= thr) and their key-order prefixes, for A and B
   constexpr int PA = kHistCap / 1024, PB = kNewCap / 1024;
   int Ka, Kb;
@@ -229,6 +235,7 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   __syncthreads();
   Ka = wsa[0];
   Kb = wsb[0];
+  OMEGA_STAMP(3);
   // 4) the merged list U, and the next sorted history (kept ones), by rank
   unsigned long long* S = p.skeys_out + (int64_t)c * p.HL;
   for (int i = tid; i < ns; i += 1024) {
@@ -242,6 +249,7 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     if ((int64_t)(uint32_t)B[j] >= thr) S[kb[j] + (r < ns ? kp[r] : Ka)] = B[j];
   }
   __syncthreads();
+  OMEGA_STAMP(4);
   // 5) split U into core / extra (a contiguous run per thread), and the gated count / sum prefixes
   // in time order over [T0 - nh, T0 + F) (a contiguous run of V per thread)
   const int G = ns + Gn;
@@ -273,6 +281,7 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   int eg, dummy_b;
   double dummy_d;
   block_excl_scan3(gi, 0, 0.0, wsa, wsb, wsd, tid, eg, dummy_b, dummy_d);
+  OMEGA_STAMP(5);
   float* core = p.core + (int64_t)c * kSeqCap;
   MeterExt* ext = p.ext + (int64_t)c * kSeqCap;
   for (int q = 0; q < pu; ++q) {
@@ -319,10 +328,12 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     p.n_s_out[c] = Ka + Kb;
     p.t0_out[c] = T0 + (uint32_t)F;
   }
+  OMEGA_STAMP(6);
   // 6) time-ordered LUFS history for the next batch (the TP history rolls in meter_query_kernel)
   const int klen = min(p.HL, L);
   for (int i = tid; i < klen; i += 1024) p.hist_l_out[(int64_t)c * p.HL + i] = V[L - klen + i];
   if (tid == 0) p.n_l_out[c] = klen;
+  OMEGA_STAMP(7);
 }
 
 __device__ __forceinline__ double lerp_pct(double a, double b, double gamma) {
@@ -434,6 +445,8 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
     out[4] = (double)tpm;
   }
 }
+
+OMEGA_STAMPS_GETTER(omega_debug_meter_stamps)
 
 // prep needs the batch's LUFS_inst only; query also reads its true peaks
 hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s) {

@@ -42,6 +42,7 @@ struct SpectralParams {
   // true peak (professional_meters.py:283-299)
   float* tp_out;      // [n_cf] or nullptr
   const float2* rot;  // [W/2 + 1] exp(+2 pi i k / (4W))
+  float4* tp_scratch;  // [n_cf, W/4] half-spectrum pairs of the 512-thread true-peak kernel (L2-resident)
   const float2* tw[kMaxLog2];  // tw[l][m] = exp(-2 pi i m / 2^l)
 };
 
@@ -58,6 +59,8 @@ struct BiquadTab {
 // the scan tables (make_biquad_tab) follows from it.
 constexpr int kw_threads(int M) { return M / 32 < 64 ? 64 : (M / 32 > 512 ? 512 : M / 32); }
 constexpr int kw_chunk(int M) { return M / kw_threads(M); }
+// the fused frame kernel (frame.hip) runs K-weighting for 16384-sample frames at 1024 threads
+constexpr int kFrameChunk = 16;
 
 struct KWeightParams {
   const float* x;
@@ -154,6 +157,14 @@ struct CombineParams {
   const int* own_rj;    // (r << 24) | j
   const float* own_frac;
   float* out;           // [n_cf, T]
+};
+
+// Segments of one mrfft_multi_kernel launch: resolution res[s] owns workgroups
+// [wg_begin[s], wg_begin[s+1]) (the last one up to the grid end).
+struct MultiPlan {
+  int n_seg;
+  int res[4];
+  int wg_begin[4];
 };
 
 struct RfftParams {

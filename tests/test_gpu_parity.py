@@ -359,15 +359,23 @@ def test_zero_frames_is_noop():
 
 def test_graph_replay_matches_direct_launch():
     """Device-memory calls are captured into HIP graphs and replayed; over several consecutive batches
-    (meter state ping-pong included) the replayed path equals direct launches bitwise."""
+    (meter state ping-pong included) the replayed path equals direct launches bitwise. The sequential
+    layout and the fused frame kernel (K-weighting in 16-sample scan chunks, another compilation of
+    the true-peak body) agree with it bitwise on spectra, within float32 rounding on TP and LUFS."""
     import torch
     from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
     from omega_gpu import _lib as L
     x = torch.from_numpy(S.cfg2_batch(8)).cuda()
     outs = []
-    for graphs in (1, 2):  # graphs + concurrent branches vs direct sequential launches
-        eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
-        eng._check(L.lib().omega_set_graphs(eng._ctx, graphs))
+    import os
+    for flags, fuse in ((1, "0"), (0, "0"), (2, "0"), (1, "1")):
+        # graphs + concurrent, direct + concurrent, direct + sequential, graphs + fused frame kernel
+        os.environ["OMEGA_FUSE"] = fuse
+        try:
+            eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+        finally:
+            del os.environ["OMEGA_FUSE"]
+        eng._check(L.lib().omega_set_graphs(eng._ctx, flags))
         bufs = [{k: torch.empty(16, *s, dtype=d, device="cuda") for k, s, d in
                  (("combined", (512,), torch.float32), ("lufs_inst", (), torch.float32),
                   ("true_peak_db", (), torch.float32), ("meters", (5,), torch.float64))} for _ in range(2)]
@@ -377,6 +385,11 @@ def test_graph_replay_matches_direct_launch():
             torch.cuda.synchronize()
             seq.append({k: v.clone() for k, v in o.items()})
         outs.append(seq)
-    for a, b in zip(*outs):
+    for a, b in zip(outs[0], outs[1]):
         for k in a:
             assert torch.equal(a[k], b[k]), k
+    for a, c in [*zip(outs[0], outs[2]), *zip(outs[0], outs[3])]:
+        assert torch.equal(a["combined"], c["combined"])
+        assert torch.max(torch.abs(a["true_peak_db"] - c["true_peak_db"])).item() < 1e-4
+        assert torch.max(torch.abs(a["lufs_inst"] - c["lufs_inst"])).item() < 1e-3
+        assert torch.max(torch.abs(a["meters"] - c["meters"])).item() < 1e-3

@@ -24,9 +24,25 @@ def main(stage):
     lib = L.lib()
     eng._bind_stream(x)
     li = torch.empty(512, device="cuda")
-    getter = {"kw": "omega_debug_kw_stamps"}[stage]
-    for _ in range(3):
-        eng._check(lib.omega_k_weighting(eng._ctx, x.data_ptr(), 512, 16384, None, li.data_ptr(), L.MEM_DEVICE))
+    getter = {"kw": "omega_debug_kw_stamps", "tp": "omega_debug_spectral_stamps",
+              "mrfft": "omega_debug_spectral_stamps", "meters": "omega_debug_meter_stamps"}[stage]
+    met = torch.empty(512, 5, dtype=torch.float64, device="cuda")
+    tpv = torch.empty(512, device="cuda")
+    comb = torch.empty(512, 512, device="cuda")
+    li.uniform_(-40, -10)
+    tpv.uniform_(-10, 0)
+    for _ in range(3 if stage != "meters" else 20):
+        if stage == "kw":
+            eng._check(lib.omega_k_weighting(eng._ctx, x.data_ptr(), 512, 16384, None, li.data_ptr(), L.MEM_DEVICE))
+        elif stage == "tp":
+            eng._check(lib.omega_true_peak(eng._ctx, x.data_ptr(), 512, 16384, li.data_ptr(), L.MEM_DEVICE))
+        elif stage == "meters":
+            eng._check(lib.omega_meter_update(eng._ctx, li.data_ptr(), tpv.data_ptr(), 256, met.data_ptr(),
+                                              L.MEM_DEVICE))
+        else:  # resolution kernels only (graphs off: the last launch is the multi-resolution kernel)
+            eng._check(lib.omega_set_graphs(eng._ctx, 2))
+            eng.process_frames(x, 256, 2 * 16384, 16384, combined=True, lufs=False, true_peak=False,
+                               out={"combined": comb})
     torch.cuda.synchronize()
     buf = np.zeros(4 * 16 * 32, np.uint64)
     fn = getattr(lib, getter)
