@@ -29,6 +29,7 @@ hipError_t launch_mrfft_independent(const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
+hipError_t launch_spectra(int m, const SpectraParams& p, int grid, hipStream_t s);
 hipError_t launch_frame(const SpectralParams& sp, const KWeightParams& kp, hipStream_t s);
 hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s);
@@ -184,6 +185,17 @@ struct omega_ctx {
   float* d_own_frac = nullptr;
   std::map<int, std::pair<double*, std::pair<int, int>>> chroma_mats;  // n_bins -> (mat, [lo, hi))
   double chroma_df = 0.0;
+  // compact chromagram tables of omega_spectra, per (n_bins, df): 5 float32 weights per bin, bins
+  // grouped by base pitch class
+  struct ChromaTab {
+    int n_bins = 0, lo = 0, hi = 0;
+    double df = 0.0;
+    float4* w4 = nullptr;
+    float* w1 = nullptr;
+    unsigned short* perm = nullptr;
+    int* goff = nullptr;
+  } ctab;
+  int n_cu = 0;
   // meter state (double-buffered)
   float* d_hist_l[2] = {};
   float* d_hist_t[2] = {};
@@ -775,6 +787,8 @@ void omega_destroy(omega_ctx* c) {
   if (c->own) (void)hipStreamSynchronize(c->own);
   for (void* p : c->allocs) (void)hipFree(p);
   for (auto& kv : c->chroma_mats) (void)hipFree(kv.second.first);
+  for (void* q : {(void*)c->ctab.w4, (void*)c->ctab.w1, (void*)c->ctab.perm, (void*)c->ctab.goff})
+    if (q) (void)hipFree(q);
   for (DevBuf& b : c->stage)
     if (b.p) (void)hipFree(b.p);
   drop_graphs(c);
@@ -1223,6 +1237,120 @@ int omega_rfft(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t windo
   p.cplx = dc;
   for (int l = 0; l < kMaxLog2; ++l) p.tw[l] = c->d_tw[l];
   HIPC(c, launch_rfft(m, p, c->stream));
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t window, omega_bands* bands,
+                  float* bands_out, double* chroma_out, float* mag_out, int mem) {
+  if (!c || !x || (!bands_out && !chroma_out && !mag_out)) return OMEGA_EINVAL;
+  if (m != 8192) return fail(c, OMEGA_EUNSUP, "spectra: frame length %d unsupported (8192)", m);
+  if (bands_out && (!bands || bands->op != OMEGA_BANDS_MAX || bands->n_bins != m / 2 + 1 || bands->n_valid > 512))
+    return fail(c, OMEGA_EINVAL, "spectra: needs a MAX band table over %d bins with at most 512 bands", m / 2 + 1);
+  if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  HIPC(c, hipSetDevice(c->device));
+  float* win = nullptr;
+  int e = get_window(c, m, window, &win);
+  if (e) return e;
+  const int nbins = m / 2 + 1;
+  const double df = (double)c->cfg.sample_rate / m;
+  if (c->ctab.n_bins != nbins || c->ctab.df != df) {
+    // chromagram.py:122-146 with offset 0: bins 20 < f < 8000, base class floor((69 + 12 log2(f/440)) mod 12)
+    int lo = nbins, hi = 0;
+    for (int k = 0; k < nbins; ++k) {
+      const double f = k * df;
+      if (f > 20 && f < 8000) {
+        lo = std::min(lo, k);
+        hi = std::max(hi, k + 1);
+      }
+    }
+    if (hi <= lo) lo = hi = 0;
+    const int nb = hi - lo;
+    if (nb > 1408) return fail(c, OMEGA_EUNSUP, "spectra: %d chroma bins (at most 1408)", nb);
+    std::vector<float4> w4(std::max(nb, 1));
+    std::vector<float> w1(std::max(nb, 1));
+    std::vector<int> base(std::max(nb, 1));
+    for (int k = lo; k < hi; ++k) {
+      const double f = k * df;
+      double cb = std::fmod(69 + 12 * std::log2(f / 440.0), 12.0);
+      if (cb < 0) cb += 12.0;
+      const int b = (int)cb;
+      const double sw = f < 100 ? 0.5 : (f < 1000 ? 1.0 : (f < 4000 ? 0.8 : 0.6));
+      float w[5];
+      for (int o = -2; o <= 2; ++o) {
+        const double d = std::fabs(cb - (b + o));
+        w[o + 2] = (float)(std::exp(-0.5 * (d / 0.5) * (d / 0.5)) * sw);
+      }
+      w4[k - lo] = make_float4(w[0], w[1], w[2], w[3]);
+      w1[k - lo] = w[4];
+      base[k - lo] = b;
+    }
+    std::vector<unsigned short> perm;
+    std::vector<int> goff(13, 0);
+    for (int b = 0; b < 12; ++b) {
+      goff[b] = (int)perm.size();
+      for (int i = 0; i < nb; ++i)
+        if (base[i] == b) perm.push_back((unsigned short)i);
+    }
+    goff[12] = (int)perm.size();
+    if (perm.empty()) perm.push_back(0);
+    for (void* q : {(void*)c->ctab.w4, (void*)c->ctab.w1, (void*)c->ctab.perm, (void*)c->ctab.goff})
+      if (q) (void)hipFree(q);
+    c->ctab = omega_ctx::ChromaTab{};
+    HIPC(c, hipMalloc(&c->ctab.w4, w4.size() * sizeof(float4)));
+    HIPC(c, hipMalloc(&c->ctab.w1, w1.size() * sizeof(float)));
+    HIPC(c, hipMalloc(&c->ctab.perm, perm.size() * sizeof(unsigned short)));
+    HIPC(c, hipMalloc(&c->ctab.goff, goff.size() * sizeof(int)));
+    HIPC(c, hipMemcpy(c->ctab.w4, w4.data(), w4.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->ctab.w1, w1.data(), w1.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->ctab.perm, perm.data(), perm.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->ctab.goff, goff.data(), goff.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->ctab.n_bins = nbins;
+    c->ctab.df = df;
+    c->ctab.lo = lo;
+    c->ctab.hi = hi;
+  }
+  if (!c->n_cu) {
+    hipDeviceProp_t prop;
+    HIPC(c, hipGetDeviceProperties(&prop, c->device));
+    c->n_cu = prop.multiProcessorCount;
+  }
+  std::vector<HostOut> outs;
+  const float* dx = x;
+  float* db = bands_out;
+  double* dcr = chroma_out;
+  float* dm = mag_out;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 0, x, (size_t)n * m * sizeof(float), reinterpret_cast<const void**>(&dx));
+    if (!e && bands_out) e = stage_out(c, 1, bands_out, (size_t)n * bands->n_out, outs, &db);
+    if (!e && chroma_out) e = stage_out(c, 2, chroma_out, (size_t)n * 12, outs, &dcr);
+    if (!e && mag_out) e = stage_out(c, 3, mag_out, (size_t)n * nbins, outs, &dm);
+    if (e) return e;
+  }
+  SpectraParams p{};
+  p.x = dx;
+  p.n = n;
+  p.stride = m;
+  p.win = win;
+  p.mag_out = dm;
+  if (bands_out) {
+    p.n_out = bands->n_out;
+    p.n_valid = bands->n_valid;
+    p.starts = bands->d_starts;
+    p.ends = bands->d_ends;
+    p.scale = bands->d_scale;
+    p.bands_out = db;
+  }
+  p.c_lo = c->ctab.lo;
+  p.c_hi = c->ctab.hi;
+  p.cw4 = c->ctab.w4;
+  p.cw1 = c->ctab.w1;
+  p.cperm = c->ctab.perm;
+  p.cgoff = c->ctab.goff;
+  p.chroma_out = dcr;
+  for (int l = 0; l < kMaxLog2; ++l) p.tw[l] = c->d_tw[l];
+  const int grid = (int)std::min<int64_t>(n, 2 * (int64_t)c->n_cu);
+  HIPC(c, launch_spectra(m, p, grid, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 }

@@ -167,6 +167,30 @@ struct MultiPlan {
   int wg_begin[4];
 };
 
+// Fused spectrum analysis (cfg3): windowed rfft magnitude (A13) -> log-band max (A10) and raw
+// chromagram (A12) of each frame, one pass over the frame.
+struct SpectraParams {
+  const float* x;
+  int64_t n, stride;       // frames of 2K samples at x + f * stride
+  const float* win;        // [2K]
+  float* mag_out;          // [n, K+1] or nullptr
+  // A10 (MAX op): bands [0, n_valid) of n_out, band i = max(mag[starts[i]:ends[i]]) * scale[i]
+  int n_out, n_valid;
+  const int* starts;
+  const int* ends;
+  const float* scale;
+  float* bands_out;        // [n, n_out] or nullptr
+  // A12: bins [c_lo, c_hi): weights of the 5 pitch classes base-2..base+2 (w4 = 5th); the bins
+  // grouped by base class: cperm[cgoff[b] .. cgoff[b+1]) = bin - c_lo of the bins with base class b
+  int c_lo, c_hi;
+  const float4* cw4;
+  const float* cw1;
+  const unsigned short* cperm;
+  const int* cgoff;        // [13]
+  double* chroma_out;      // [n, 12] or nullptr (smoothed, normalised; before the temporal blend)
+  const float2* tw[kMaxLog2];
+};
+
 struct RfftParams {
   const float* x;
   int64_t n;

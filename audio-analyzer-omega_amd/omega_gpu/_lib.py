@@ -61,6 +61,8 @@ EXPORTS = {
                                        C.POINTER(Outputs), C.c_int]),
     "omega_process_stream": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int64,
                                        C.POINTER(Outputs), C.c_int, C.POINTER(C.c_int64)]),
+    "omega_spectra": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                                C.c_void_p, C.c_void_p, C.c_int]),
     "omega_combine": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int64, C.c_void_p, C.c_int]),
     "omega_true_peak": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int]),
     "omega_k_weighting": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p,

@@ -217,6 +217,30 @@ class Engine:
                                        cp.ctypes.data if cp is not None else None, L.MEM_HOST))
         return mag, cp
 
+    def spectra(self, x, window: str = "hann", bands: Optional["BandTable"] = None, chroma: bool = True,
+                mags: bool = False, out: Optional[Dict] = None) -> Dict:
+        """Fused cfg3 analysis (omega_spectra) of frames x [n, 8192] (host numpy or device torch):
+        'bands' [n, n_out] (A10 without smoothing, needs a MAX BandTable over 4097 bins), 'chroma'
+        [n, 12] (A12 before the temporal blend), 'mag' [n, 4097] (A13 magnitude)."""
+        dev = _is_torch(x)
+        if not dev:
+            x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float32)
+        n, m = x.shape
+        o = dict(out or {})
+        if bands is not None and "bands" not in o:
+            o["bands"] = self._alloc(x, (n, bands.n_out), np.float32)
+        if chroma and "chroma" not in o:
+            o["chroma"] = self._alloc(x, (n, 12), np.float64)
+        if mags and "mag" not in o:
+            o["mag"] = self._alloc(x, (n, m // 2 + 1), np.float32)
+        if dev:
+            self._bind_stream(x)
+        self._check(L.lib().omega_spectra(self._ctx, _ptr(x), n, m, L.WIN.get(window, 1),
+                                          bands._h if bands is not None else None, _ptr(o.get("bands")),
+                                          _ptr(o.get("chroma")), _ptr(o.get("mag")),
+                                          L.MEM_DEVICE if dev else L.MEM_HOST))
+        return o
+
     def chroma_raw(self, spec: np.ndarray, df: float) -> np.ndarray:
         s = np.ascontiguousarray(np.atleast_2d(spec), dtype=np.float32)
         out = np.empty((s.shape[0], 12), np.float64)

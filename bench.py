@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 (HBM-roofline) line")
     return ap.parse_args()
 
 
@@ -77,6 +78,57 @@ def kernel_time_ms(eng, xd, reps=20):
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / reps, ncf
+
+
+def cfg3_line(dev, reps=20):
+    """BASELINE cfg3, the HBM-roofline run: 4096 mono frames x 8192 samples, fused windowed rfft ->
+    512 log bands + 12-bin chromagram (omega_spectra), one launch per batch, inputs resident in HBM.
+    Bytes per frame from SURVEY.md §8(d): 4 * 8192 in + 4 * (512 + 12) out = 34,864."""
+    from omega_gpu import Engine, Resolution
+    from omega_gpu import _lib as L
+    from omega_gpu.engine import BandTable
+    n, m = 4096, 8192
+    x = torch.from_numpy(cfg3_input(n, m)).to(dev)
+    eng = Engine([Resolution((20, 20000), m, m // 4, 1.0)], FS, 20000, 512, device=dev.index or 0)
+    st, en, comp = band_table_512()
+    bt = BandTable(eng, L.BANDS_MAX, st, en, 512, m // 2 + 1, scale=comp)
+    out = {"bands": torch.empty(n, 512, device=dev), "chroma": torch.empty(n, 12, dtype=torch.float64, device=dev)}
+    for _ in range(3):
+        eng.spectra(x, "hann", bands=bt, chroma=True, out=out)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        eng.spectra(x, "hann", bands=bt, chroma=True, out=out)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    bpf = 4 * m + 4 * (512 + 12)
+    gbs = n * bpf / (ms * 1e-3) / 1e9
+    return {"workload": "cfg3: 4096 mono frames x 8192, Hann rfft -> 512 log bands (A10) + chromagram (A12), fused",
+            "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_batch": ms,
+            "roofline": {"bound": "hbm", "kernel": "spectra_kernel<4096>", "achieved": gbs, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
+                         "bytes_per_frame": bpf}}
+
+
+def cfg3_input(n, m):
+    """BASELINE cfg3 synthetic frames (same generator as oracle/signals.cfg3_batch): even frames a
+    0.5-amplitude C-major triad, odd frames 0.1 N(0,1) (seed 1234)."""
+    t = np.arange(m) / FS
+    tri = (0.5 * (np.sin(2 * np.pi * 261.63 * t) + np.sin(2 * np.pi * 329.63 * t) +
+                  np.sin(2 * np.pi * 392.00 * t))).astype(np.float32)
+    nz = (0.1 * np.random.default_rng(1234).standard_normal((n // 2 + 1) * m)).astype(np.float32).reshape(-1, m)
+    out = np.empty((n, m), np.float32)
+    out[0::2] = tri
+    out[1::2] = nz[: n // 2]
+    return out
+
+
+def band_table_512(fs=FS, num_bands=512, fft_size=8192):
+    """AudioProcessingPipeline band table (pipeline.py:165-230) via the product facade."""
+    from omega_gpu.bands import pipeline_band_table
+    return pipeline_band_table(fs, num_bands, fft_size)
 
 
 def tp_traffic():
@@ -215,6 +267,8 @@ def main():
                                  "launch stream"},
             "cpu_baseline": cpu,
         }
+        if world == 1 and not a.no_cfg3:
+            line["cfg3"] = cfg3_line(dev)
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -23,6 +23,7 @@
  *                          PrecomputedFrequencyMapper.map_spectrum_to_bars omega4/optimization/freq_mapper.py:165-196 (mean-reduce)
  *   omega_chroma           ChromagramAnalyzer.compute_chromagram      omega4/panels/chromagram.py:109-159
  *   omega_rfft             BatchedFFTProcessor process_batch (CPU/CuPy branches) omega4/optimization/batched_fft_processor.py:148-285
+ *   omega_spectra          omega_rfft -> omega_bands_apply (MAX) + omega_chroma fused in one pass (cfg3)
  *
  * Conventions:
  *   - every function returns 0 on success and a negative omega_status on error; the message is
@@ -176,6 +177,15 @@ int omega_chroma(omega_ctx* ctx, const float* spec, int64_t n, int32_t n_bins, d
 /* ---- windowed R2C FFT (A13): magnitude [n, m/2+1] and/or complex [n, m/2+1] (interleaved) ---- */
 int omega_rfft(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t window, float* mag,
                float* cplx, int mem);
+
+/* ---- fused spectrum analysis (BASELINE cfg3): per frame of m samples (m = 8192), the windowed
+ * rfft magnitude (A13), the log-band max of a MAX band table (A10, before smoothing; bands may be
+ * NULL) and the chromagram before its temporal blend (A12, bins at df = sample_rate / m), reading
+ * each frame once. Any output may be NULL: bands_out [n, n_out], chroma_out [n, 12], mag_out
+ * [n, m/2+1]. Replaces the BatchedFFTProcessor -> map_to_bands / compute_chromagram chain
+ * (batched_fft_processor.py:148-285, pipeline.py:295-335, chromagram.py:109-159). ---- */
+int omega_spectra(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t window, omega_bands* bands,
+                  float* bands_out, double* chroma_out, float* mag_out, int mem);
 
 #ifdef __cplusplus
 }

@@ -15,3 +15,9 @@ def test_bench_algorithmic_figures():
     assert round(bench.FLOP_FFT / 1e6, 2) == 1.09
     assert round(bench.FLOP_KW / 1e6, 2) == 0.67
     assert bench.BYTES_CF == 67592
+
+
+def test_cfg3_input_matches_oracle_generator():
+    import bench
+    from oracle import signals as S
+    np.testing.assert_array_equal(bench.cfg3_input(8, 8192), S.cfg3_batch(8))

@@ -393,3 +393,55 @@ def test_graph_replay_matches_direct_launch():
         assert torch.max(torch.abs(a["true_peak_db"] - c["true_peak_db"])).item() < 1e-4
         assert torch.max(torch.abs(a["lufs_inst"] - c["lufs_inst"])).item() < 1e-3
         assert torch.max(torch.abs(a["meters"] - c["meters"])).item() < 1e-3
+
+
+def test_spectra_cfg3_vs_oracle():
+    """cfg3 fused analysis (omega_spectra): Hann rfft magnitude (A13) -> 512 log bands (A10) and the
+    raw chromagram (A12) of alternating triad / noise frames, against the oracle chain. Tolerances:
+    magnitudes 1e-4 normwise (north star), bands 1e-4 relative, chroma 1e-5 relative (float32
+    projection weights instead of the reference's float64 matrix)."""
+    from omega_gpu import Engine, Resolution
+    from omega_gpu.engine import BandTable
+    from omega_gpu import _lib as L
+    x = S.cfg3_batch(16)
+    eng = Engine([Resolution((20, 20000), 8192, 2048, 1.0)], FS, 20000, 512)
+    st, en, comp = R.pipeline_band_table(FS, 512, 8192)
+    bt = BandTable(eng, L.BANDS_MAX, st, en, 512, 4097, scale=comp)
+    out = eng.spectra(x, "hann", bands=bt, chroma=True, mags=True)
+    freqs = np.fft.rfftfreq(8192, 1 / FS)
+    for f in range(len(x)):
+        mag = R.batched_fft(x[f], 8192, "hann")["magnitude"]
+        assert normwise(out["mag"][f], mag) < SPEC_TOL
+        bands = R.map_to_bands(mag.astype(np.float32), st, en, comp, 512)
+        np.testing.assert_allclose(out["bands"][f], bands, rtol=1e-4, atol=1e-6 * np.max(bands))
+        ch = R.ChromaState().compute(mag.astype(np.float32), freqs)
+        np.testing.assert_allclose(out["chroma"][f], ch, rtol=1e-5, atol=1e-9)
+    # the band stage equals the standalone A10 entry point on the same magnitudes
+    np.testing.assert_array_equal(out["bands"], bt.apply(out["mag"]))
+
+
+def test_cfg5_stream_96k_surround():
+    """BASELINE cfg5 shape at small size: 96 kHz, 8 channels, stream layout (hop 1024) of 16384-point
+    frames with true peak, K-weighted LUFS (filters designed for 96 kHz) and the meter aggregates,
+    against the oracle per channel (a few frames of each channel's stream)."""
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    fs, C, W, H, F = 96000, 8, 16384, 1024, 6
+    n = W + H * (F - 1)
+    t = np.arange(n) / fs
+    x = np.stack([(0.2 * np.sin(2 * np.pi * 110 * (c + 1) * t)).astype(np.float32) +
+                  S.noise(c, n, 0.02) for c in range(C)]).astype(np.float32)
+    eng = Engine(NORTHSTAR_RESOLUTIONS, fs, 20000, target_bins=512, n_channels=C)
+    out = eng.process_stream(x.ravel(), n, H, channel_stride=n, combined=True, meters=True)
+    assert out["lufs_inst"].shape == (F * C,)
+    for c in (0, 3, 7):
+        st = R.MeterState(fs)
+        for f in range(F):
+            fr = x[c, f * H:f * H + W]
+            _, comb, li, tp = R.full_frame(fr, fs=fs)
+            cf = f * C + c
+            assert normwise(out["combined"][cf], comb) < SPEC_TOL
+            assert abs(out["lufs_inst"][cf] - li) < LU_TOL
+            assert abs(out["true_peak_db"][cf] - tp) < TP_TOL_DB
+            agg = np.array(list(st.update(fr, li, tp).values()))
+            assert np.all(np.abs(out["meters"][cf][:4] - agg[:4]) < LU_TOL)
+            assert abs(out["meters"][cf][4] - agg[4]) < TP_TOL_DB

@@ -25,7 +25,15 @@ def main(stage):
     eng._bind_stream(x)
     li = torch.empty(512, device="cuda")
     getter = {"kw": "omega_debug_kw_stamps", "tp": "omega_debug_spectral_stamps",
-              "mrfft": "omega_debug_spectral_stamps", "meters": "omega_debug_meter_stamps"}[stage]
+              "mrfft": "omega_debug_spectral_stamps", "meters": "omega_debug_meter_stamps",
+              "spectra": "omega_debug_spectra_stamps"}[stage]
+    if stage == "spectra":
+        from omega_gpu import Resolution
+        from omega_gpu.engine import BandTable
+        x3 = torch.from_numpy(bench.cfg3_input(4096, 8192)).cuda()
+        e3 = Engine([Resolution((20, 20000), 8192, 2048, 1.0)], 48000, 20000, 512)
+        st_, en_, comp_ = bench.band_table_512()
+        bt = BandTable(e3, L.BANDS_MAX, st_, en_, 512, 4097, scale=comp_)
     met = torch.empty(512, 5, dtype=torch.float64, device="cuda")
     tpv = torch.empty(512, device="cuda")
     comb = torch.empty(512, 512, device="cuda")
@@ -36,6 +44,8 @@ def main(stage):
             eng._check(lib.omega_k_weighting(eng._ctx, x.data_ptr(), 512, 16384, None, li.data_ptr(), L.MEM_DEVICE))
         elif stage == "tp":
             eng._check(lib.omega_true_peak(eng._ctx, x.data_ptr(), 512, 16384, li.data_ptr(), L.MEM_DEVICE))
+        elif stage == "spectra":
+            e3.spectra(x3, "hann", bands=bt, chroma=True)
         elif stage == "meters":
             eng._check(lib.omega_meter_update(eng._ctx, li.data_ptr(), tpv.data_ptr(), 256, met.data_ptr(),
                                               L.MEM_DEVICE))
