@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one stage of the cfg2 hot path in isolation (for rocprofv3 counter passes and A/B timing).
 
-  python tools/kernel_bench.py {tp,kw,mrfft,meters,all,host} [--reps N]
+  python tools/kernel_bench.py {tp,kw,mrfft,meters,all,host,spectra} [--reps N]
 """
 import argparse
 import os
@@ -35,8 +35,19 @@ def main():
 
     xh = bench.cfg2_input()
     host_out = {}
+    if a.stage == "spectra":
+        from omega_gpu import Resolution
+        from omega_gpu.engine import BandTable
+        x3 = torch.from_numpy(bench.cfg3_input(4096, 8192)).cuda()
+        e3 = Engine([Resolution((20, 20000), 8192, 2048, 1.0)], 48000, 20000, 512)
+        st_, en_, comp_ = bench.band_table_512()
+        bt = BandTable(e3, L.BANDS_MAX, st_, en_, 512, 4097, scale=comp_)
+        so = {"bands": torch.empty(4096, 512, device="cuda"),
+              "chroma": torch.empty(4096, 12, dtype=torch.float64, device="cuda")}
 
     def run():
+        if a.stage == "spectra":
+            e3.spectra(x3, "hann", bands=bt, chroma=True, out=so)
         if a.stage == "host":  # host buffers in and out: PCIe-inclusive rate of the full path
             host_out.update(eng.process_frames(xh, 256, 2 * 16384, 16384, meters=True))
         if a.stage in ("tp", "all"):
