@@ -125,6 +125,12 @@ BiquadTab make_biquad_tab(const BiquadCoef& c, int L) {
     }
     if (n + 1 <= L) mat2_mul(A, An, An);
   }
+  // A^(L / kKwSub) for the sub-chunks of one thread's chunk
+  {
+    double As[4] = {1, 0, 0, 1};
+    for (int n = 0; n < L / kKwSub; ++n) mat2_mul(A, As, As);
+    for (int q = 0; q < 4; ++q) t.psub[q] = (float)As[q];
+  }
   // An = A^L now (L <= 64)
   double P[4];
   std::memcpy(P, An, sizeof P);
@@ -154,8 +160,13 @@ struct omega_ctx {
   // fork/join streams + events for the concurrent branches, and the graph cache
   hipStream_t cap = nullptr, fork[2] = {nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
-  bool use_graph = true;
-  bool concurrent = true;   // overlap the latency-bound stages (small FFTs, meters) with full-chip ones
+  // HIP graph replay of device-memory calls: off by default -- on MI355X (ROCm 7) a replayed graph
+  // put the stream layout's nodes on other queues, with ~12 us cross-queue waits and ~20 us between
+  // consecutive launches (cfg2 step 149.5 us vs 128.8 us for direct launches of the same layout)
+  bool use_graph = false;
+  // stream layout of the per-batch work (enqueue_frames): 0 sequential, 1 concurrent branches,
+  // 2 sequential full-chip kernels with the meter aggregates on a side stream
+  int layout = 2;
   bool res_independent = false;  // no combine target has several owners: resolution kernels commute
   hipEvent_t ev_kw = nullptr;
   struct GraphEntry {
@@ -607,11 +618,10 @@ int finish_host(omega_ctx* c, const std::vector<HostOut>& outs) {
 
 // Meter aggregates over n_frames x C values, in chunks of at most kChunkFrames frames; each chunk
 // reads the state buffers `cur` and writes `cur ^ 1`.
-// tp_ready: when set, an event the true peaks of the batch wait on (the prep kernels only read the
-// LUFS_inst values, so they may start before it).
-int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_frames, double* out,
-                   hipStream_t stream, hipEvent_t tp_ready) {
+std::vector<MeterPrepParams> meter_chunks(omega_ctx* c, const float* lufs, const float* tp, int64_t n_frames,
+                                          double* out) {
   const int C = c->cfg.n_channels;
+  std::vector<MeterPrepParams> v;
   for (int64_t f0 = 0; f0 < n_frames; f0 += kChunkFrames) {
     const int64_t nf = std::min<int64_t>(kChunkFrames, n_frames - f0);
     const int a = c->cur, b = c->cur ^ 1;
@@ -648,19 +658,32 @@ int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_f
     p.gcount = c->d_gcount;
     p.gsum = c->d_gsum;
     p.out = out + f0 * C * OMEGA_N_METERS;
-    HIPC(c, launch_meter_prep(p, stream));
-    if (tp_ready && f0 == 0) HIPC(c, hipStreamWaitEvent(stream, tp_ready, 0));
-    HIPC(c, launch_meter_query(p, stream));
+    p.parts = 3;
+    v.push_back(p);
     c->cur = b;
+  }
+  return v;
+}
+
+// All meter chunks on one stream. tp_ready: when set, an event the true peaks of the batch wait on
+// (the prep kernels only read the LUFS_inst values, so they may start before it).
+int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_frames, double* out,
+                   hipStream_t stream, hipEvent_t tp_ready) {
+  bool first = true;
+  for (const MeterPrepParams& p : meter_chunks(c, lufs, tp, n_frames, out)) {
+    HIPC(c, launch_meter_prep(p, stream));
+    if (tp_ready && first) HIPC(c, hipStreamWaitEvent(stream, tp_ready, 0));
+    HIPC(c, launch_meter_query(p, stream));
+    first = false;
   }
   return 0;
 }
 
-// The per-batch work. Sequential: resolution kernels, true peak, K-weighting, meters on `s`.
-// Concurrent (default): true peak on fork[1] and the resolution kernels (in resolution order) on
-// fork[0] from the start; K-weighting and then the meter aggregates' prep kernel (it needs the batch's
+// The per-batch work (c->layout). 0 sequential: resolution kernels, true peak, K-weighting, meters on
+// `s`. 1 concurrent: true peak on fork[1] and the resolution kernels (in resolution order) on fork[0]
+// from the start; K-weighting and then the meter aggregates' prep kernel (it needs the batch's
 // LUFS_inst only) on `s`, whose query kernel then waits for the true peaks; both branches join back
-// into `s`.
+// into `s`. 2 (default): see below.
 // kp16: the K-weighting parameters with 16-sample-chunk tables for the fused frame kernel (hp null
 // when not built).
 int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, const KWeightParams& kp16, int W,
@@ -668,7 +691,7 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
   const bool do_tp = sp.tp_out != nullptr, do_kw = kp.lufs_out || kp.weighted_out;
   const bool do_res = sp.comb_out != nullptr || sp.res[0].mag_out || sp.res[1].mag_out || sp.res[2].mag_out ||
                       sp.res[3].mag_out;
-  if (!c->concurrent) {
+  if (c->layout == 0) {
     if (do_res) HIPC(c, c->res_independent ? launch_mrfft_independent(sp, s) : launch_mrfft(sp, s));
     if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
     if (do_kw) HIPC(c, launch_kweight(W, kp, s));
@@ -688,6 +711,34 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
       if (e) return e;
     }
     if (do_res) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
+    return 0;
+  }
+  if (c->layout == 2) {
+    // the full-chip kernels back to back on `s` (K-weighting first); the meter aggregates' prep and
+    // LUFS query kernels (one or two workgroups per channel: latency-bound) run on fork[0] beside the
+    // resolution and true-peak kernels, the true-peak meter after the true peaks on `s`. (Concurrent
+    // full-chip kernels lose to this: 512 channel-frames are exactly two rounds of 256 CUs, and a CU
+    // held by another kernel pushes a third round.)
+    if (do_kw) HIPC(c, launch_kweight(W, kp, s));
+    std::vector<MeterPrepParams> mc;
+    if (meters) {
+      mc = meter_chunks(c, lufs, tp, n_frames, meters);
+      HIPC(c, hipEventRecord(c->ev_kw, s));
+      HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_kw, 0));
+      for (MeterPrepParams p : mc) {
+        HIPC(c, launch_meter_prep(p, c->fork[0]));
+        p.parts = 1;
+        HIPC(c, launch_meter_query(p, c->fork[0]));
+      }
+      HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
+    }
+    if (do_res) HIPC(c, c->res_independent ? launch_mrfft_independent(sp, s) : launch_mrfft(sp, s));
+    if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
+    for (MeterPrepParams p : mc) {
+      p.parts = 2;
+      HIPC(c, launch_meter_query(p, s));
+    }
+    if (meters) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
     return 0;
   }
   if (do_tp) {
@@ -759,9 +810,10 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   c->stream = c->own;
   if (const char* fz = std::getenv("OMEGA_FUSE")) c->fuse_frame = std::atoi(fz) != 0;
   if (const char* tl = std::getenv("OMEGA_TP_L2")) c->tp_l2 = std::atoi(tl) != 0;
+  if (const char* gr = std::getenv("OMEGA_GRAPHS")) c->use_graph = std::atoi(gr) != 0;
   if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
     const int v = std::atoi(lay);
-    c->concurrent = v != 0;
+    c->layout = v < 0 || v > 2 ? 2 : v;
   }
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking);
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->fork[0], hipStreamNonBlocking);
@@ -812,7 +864,8 @@ int omega_set_stream(omega_ctx* c, void* s) {
 int omega_set_graphs(omega_ctx* c, int enable) {
   if (!c) return OMEGA_EINVAL;
   c->use_graph = (enable & 1) != 0;
-  c->concurrent = (enable & 2) == 0;
+  const int lay = (enable >> 1) & 3;  // 0 default, 1 sequential, 2 concurrent branches, 3 meters aside
+  c->layout = lay == 0 ? 2 : lay - 1;
   drop_graphs(c);
   return 0;
 }

@@ -12,6 +12,7 @@ namespace omega {
 struct BqRegs {
   float b0, a1, a2, B0, B1, zi0, zi1;
   float4 p1, p2, p4, p8, p64;  // P, P^2, P^4, P^8, P^64
+  float4 ps;                   // A^(L / kKwSub)
 };
 
 __device__ __forceinline__ float4 ld4(const float* q) { return make_float4(q[0], q[1], q[2], q[3]); }
@@ -30,6 +31,7 @@ __device__ __forceinline__ BqRegs bq_regs(const BiquadTab* __restrict__ t) {
   r.p4 = ld4(t->pw[3]);
   r.p8 = ld4(t->pw[7]);
   r.p64 = ld4(t->pw[63]);
+  r.ps = ld4(t->psub);
   return r;
 }
 
@@ -80,11 +82,28 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
   const int lane = tid & 63, wv = tid >> 6;
   const int vl = REV ? 63 - lane : lane;       // position in processing order within the wave
   const int vw = REV ? NW - 1 - wv : wv;       // wave position in processing order
-  // 1) zero-state end state of the chunk (outputs come in step 5)
-  float s0 = 0.f, s1 = 0.f;
-  static_for<0, L>([&](auto i) {
-    constexpr int n = REV ? L - 1 - i : i;
-    bq_state(t, u[n], s0, s1);
+  // 1) zero-state end state of the chunk (outputs come in step 5): kKwSub sub-chunks of LS samples
+  // run interleaved from zero (independent chains), then folded in processing order with A^LS
+  constexpr int S = (L % kKwSub == 0 && L >= 2 * kKwSub) ? kKwSub : 1;
+  constexpr int LS = L / S;
+  float e0[S], e1[S];
+  static_for<0, S>([&](auto j) {
+    e0[j] = 0.f;
+    e1[j] = 0.f;
+  });
+  static_for<0, LS>([&](auto i) {
+    static_for<0, S>([&](auto j) {
+      // sub-chunk j in processing order covers samples (REV: from the end) j*LS .. j*LS + LS - 1
+      constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
+      bq_state(t, u[n], e0[j], e1[j]);
+    });
+  });
+  float s0 = e0[0], s1 = e1[0];
+  static_for<1, S>([&](auto j) {
+    float r0, r1;
+    mv4(t.ps, s0, s1, r0, r1);
+    s0 = r0 + e0[j];
+    s1 = r1 + e1[j];
   });
   OMEGA_STAMP(SB);
   // 2) inclusive scan of the chunk end states in processing order, S_l += P^d S_{l-d}: within rows
@@ -155,12 +174,23 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
   const float i0 = vl == 0 ? k0 : p0;
   const float i1 = vl == 0 ? k1 : p1;
   OMEGA_STAMP(SB + 3);
-  // 5) the chunk from its true incoming state
+  // 5) the chunk from its true incoming state: each sub-chunk's incoming state follows from the
+  // previous one's (A^LS in + its zero-state end state), then all run interleaved
   {
-    float r0 = i0, r1 = i1;
-    static_for<0, L>([&](auto i) {
-      constexpr int n = REV ? L - 1 - i : i;
-      u[n] = bq_step(t, u[n], r0, r1);
+    float r0[S], r1[S];
+    r0[0] = i0;
+    r1[0] = i1;
+    static_for<1, S>([&](auto j) {
+      float q0, q1;
+      mv4(t.ps, r0[j - 1], r1[j - 1], q0, q1);
+      r0[j] = q0 + e0[j - 1];
+      r1[j] = q1 + e1[j - 1];
+    });
+    static_for<0, LS>([&](auto i) {
+      static_for<0, S>([&](auto j) {
+        constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
+        u[n] = bq_step(t, u[n], r0[j], r1[j]);
+      });
     });
   }
   OMEGA_STAMP(SB + 4);

@@ -28,8 +28,16 @@ OMEGA_STAMPS_DECL
 
 namespace omega {
 
+// OMEGA_KW_WG_PER_CU: workgroups per CU the register budget is sized for (0: compiler's choice); two
+// 512-thread workgroups per CU (128 VGPRs, a few spilled loop invariants) measured 22.3 us vs 25.4 us
+// for one (134 VGPRs) on the cfg2 batch
+#ifndef OMEGA_KW_WG_PER_CU
+#define OMEGA_KW_WG_PER_CU 2
+#endif
+constexpr int kw_waves_per_eu(int nth) { return OMEGA_KW_WG_PER_CU * nth / 256 > 0 ? OMEGA_KW_WG_PER_CU * nth / 256 : 1; }
+
 template <int M, int NTH = kw_threads(M)>
-__global__ __launch_bounds__(NTH) void kweight_kernel(KWeightParams p) {
+__global__ __launch_bounds__(NTH, kw_waves_per_eu(NTH)) void kweight_kernel(KWeightParams p) {
   constexpr int NW = NTH / 64;
   static_assert(M / NTH == kw_chunk(M), "chunk length must match the host tables");
   __shared__ float4 pwl[2][64];  // P^(l+1) of both filters, for the lane-indexed step of the scan

@@ -346,14 +346,17 @@ __device__ __forceinline__ float seq_at(const float* hist, const float* batch, i
   return i < nh ? hist[(int64_t)c * HC + i] : batch[(i - nh) * C + c];
 }
 
-// One wave per output (f, c); workgroup (0, c) also rolls the channel's true-peak history.
+// One wave per output (f, c); workgroup (0, c) also rolls the channel's true-peak history. parts
+// selects the LUFS meters (they need the prep kernel's output) and/or the true-peak meter (it needs the
+// batch's true peaks only), so the two can run on different streams.
 __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.y;
   const int C = p.C;
   const int nt = p.n_t_in[c];
   const int64_t F = p.n_frames;
-  if (blockIdx.x == 0) {
+  const bool do_l = p.parts & 1, do_t = p.parts & 2;
+  if (blockIdx.x == 0 && do_t) {
     const int64_t tt = (int64_t)nt + F;
     const int ktl = (int)min<int64_t>(p.HT, tt);
     for (int i = threadIdx.x; i < ktl; i += 256) {
@@ -364,6 +367,14 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
   }
   const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= F) return;
+  if (do_t) {
+    const int64_t ntp = nt + f + 1, wt = min<int64_t>(p.peak_len, ntp);
+    float tpm = -INFINITY;
+    for (int64_t i = lane; i < wt; i += 64) tpm = fmaxf(tpm, seq_at(p.hist_t_in, p.tp, nt, p.HT, C, c, ntp - wt + i));
+    tpm = wave_max(tpm);
+    if (lane == 0) p.out[(f * C + c) * 5 + 4] = (double)tpm;
+  }
+  if (!do_l) return;
   const int nh = p.n_l_in[c];
   const uint32_t T0 = p.t0_in[c];
   const int64_t n = nh + f + 1;  // the sequence known to this frame, local index 0 = absolute T0 - nh
@@ -432,17 +443,12 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
       if (!found[w]) val[w] = core[want[w] - below[w]];
     range = lerp_pct(val[2], val[3], gam[1]) - lerp_pct(val[0], val[1], gam[0]);
   }
-  const int64_t ntp = nt + f + 1, wt = min<int64_t>(p.peak_len, ntp);
-  float tpm = -INFINITY;
-  for (int64_t i = lane; i < wt; i += 64) tpm = fmaxf(tpm, seq_at(p.hist_t_in, p.tp, nt, p.HT, C, c, ntp - wt + i));
-  tpm = wave_max(tpm);
   if (lane == 0) {
     double* out = p.out + (f * C + c) * 5;
     out[0] = sm / (double)wm;
     out[1] = ss / (double)ws;
     out[2] = integ;
     out[3] = range;
-    out[4] = (double)tpm;
   }
 }
 

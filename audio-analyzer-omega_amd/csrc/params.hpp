@@ -53,7 +53,14 @@ struct BiquadTab {
   float zi0, zi1;      // scipy.signal.lfilter_zi
   float h0[64], h1[64];  // first row of A^n, n < L (zero-input response of a chunk)
   float pw[64][4];     // P^(l+1), P = A^L, row-major 2x2
+  float psub[4];       // A^(L / kKwSub): the sub-chunk step inside one thread's chunk
 };
+
+// each thread runs its chunk as kKwSub interleaved sub-chunks (independent recurrences: ILP)
+#ifndef OMEGA_KW_SUB
+#define OMEGA_KW_SUB 1
+#endif
+constexpr int kKwSub = OMEGA_KW_SUB;
 
 // K-weighting workgroup: up to 32 samples per thread (M/32 threads, 64..512), the chunk length L of
 // the scan tables (make_biquad_tab) follows from it.
@@ -120,6 +127,7 @@ struct MeterPrepParams {
   int* gcount;      // [C, kMeterSeqCap + 1] gated-count prefix in time order
   double* gsum;     // [C, kMeterSeqCap + 1] gated-sum prefix in time order
   double* out;                     // [n_frames * C, 5]
+  int parts;  // meter_query_kernel: bit 0 the LUFS meters (columns 0-3), bit 1 the true-peak meter (4)
 };
 
 struct BandParams {

@@ -10,6 +10,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libomega.so")
 if os.environ.get("OMEGA_STAMPS_BUILD") == "1":  # kernel-development build (make stamps), tools/stamps.py
     LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libomega_stamps.so")
+elif os.environ.get("OMEGA_VARIANT"):  # kernel-development variant (make variant VAR=...)
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", f"var_{os.environ['OMEGA_VARIANT']}.so")
 
 MAX_RES = 4
 N_METERS = 5

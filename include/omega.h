@@ -114,11 +114,12 @@ const char* omega_version(void);
 /* Enqueue on a caller-owned hipStream_t (NULL = the null/default stream, e.g. PyTorch's default
  * stream). Contexts start on a private non-blocking stream. */
 int omega_set_stream(omega_ctx* ctx, void* hip_stream);
-/* Device-memory omega_process_frames calls are captured once per distinct argument set into a HIP
- * graph (three branches: resolution kernels / true peak / K-weighting, joined before the
- * meter aggregates) and replayed afterwards. flags: bit 0 = use graphs (default on); bit 1 = run
- * everything sequentially on one stream (default off: the latency-bound stages -- smaller resolutions,
- * meter aggregates -- overlap the full-chip true-peak / K-weighting / largest-resolution kernels). */
+/* flags: bit 0 = HIP graphs: device-memory omega_process_frames calls are captured once per distinct
+ * argument set and replayed afterwards (default off: measured slower than direct launches on MI355X,
+ * see DESIGN.md); bits 1-2 = stream layout:
+ * 0 default (= 3), 1 everything sequentially on one stream, 2 three concurrent branches (resolution
+ * kernels / true peak / K-weighting + meters), 3 the full-chip kernels sequentially with the
+ * latency-bound meter aggregates on a side stream. */
 int omega_set_graphs(omega_ctx* ctx, int flags);
 int omega_synchronize(omega_ctx* ctx);
 

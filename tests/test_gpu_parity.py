@@ -350,6 +350,36 @@ def test_stream_layout_hop(cfg2):
     assert eng2.process_stream(s, W - 1, H)["combined"].shape == (0, 256)
 
 
+def test_meter_chunks_across_layouts():
+    """A batch longer than one meter chunk (kMeterChunk = 2048 frames): the default layout (meter
+    prep + LUFS meters on a side stream, the true-peak meter on the main one, chunk by chunk) gives
+    the sequential layout's meters bitwise, and a frame past the chunk boundary matches the oracle's
+    sequential calculate_lufs calls."""
+    import torch
+    from omega_gpu import Engine, Resolution
+    from omega_gpu import _lib as L
+    W, H, F = 1024, 64, 2100
+    n = W + H * (F - 1)
+    x = torch.from_numpy(np.stack([S.sine(330, 0.3, n) * (1 + 0.5 * np.sin(np.arange(n) / 9000.0)),
+                                   S.noise(5, n, 0.1)]).astype(np.float32).ravel()).cuda()
+    res = []
+    for flags in (1, 2, 0):  # graphs + default, direct + sequential, direct + default
+        eng = Engine([Resolution((20, 20000), 1024, 256, 1.0)], FS, 20000, 64, n_channels=2)
+        eng._check(L.lib().omega_set_graphs(eng._ctx, flags))
+        o = eng.process_stream(x, n, H, channel_stride=n, combined=False, meters=True)
+        torch.cuda.synchronize()
+        res.append({k: v.cpu().numpy() for k, v in o.items()})
+    for r in res[1:]:
+        for k in res[0]:
+            np.testing.assert_array_equal(res[0][k], r[k], err_msg=k)
+    li = res[0]["lufs_inst"].reshape(F, 2)
+    tp = res[0]["true_peak_db"].reshape(F, 2)
+    st = R.MeterState(FS)
+    for f in range(F):
+        agg = st.update(np.ones(1), float(li[f, 1]), float(tp[f, 1]))
+    np.testing.assert_allclose(res[0]["meters"].reshape(F, 2, 5)[F - 1, 1], list(agg.values()), rtol=0, atol=1e-9)
+
+
 def test_zero_frames_is_noop():
     from omega_gpu import Engine, Resolution
     e = Engine([Resolution((20, 20000), 1024, 256, 1.0)], FS, 20000, 16)
@@ -368,8 +398,9 @@ def test_graph_replay_matches_direct_launch():
     x = torch.from_numpy(S.cfg2_batch(8)).cuda()
     outs = []
     import os
-    for flags, fuse in ((1, "0"), (0, "0"), (2, "0"), (1, "1")):
-        # graphs + concurrent, direct + concurrent, direct + sequential, graphs + fused frame kernel
+    for flags, fuse in ((1, "0"), (0, "0"), (2, "0"), (1, "1"), (5, "0")):
+        # graphs + default layout (meters on a side stream), direct + default, direct + sequential,
+        # graphs + fused frame kernel, graphs + three concurrent branches
         os.environ["OMEGA_FUSE"] = fuse
         try:
             eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
@@ -388,7 +419,7 @@ def test_graph_replay_matches_direct_launch():
     for a, b in zip(outs[0], outs[1]):
         for k in a:
             assert torch.equal(a[k], b[k]), k
-    for a, c in [*zip(outs[0], outs[2]), *zip(outs[0], outs[3])]:
+    for a, c in [*zip(outs[0], outs[2]), *zip(outs[0], outs[3]), *zip(outs[0], outs[4])]:
         assert torch.equal(a["combined"], c["combined"])
         assert torch.max(torch.abs(a["true_peak_db"] - c["true_peak_db"])).item() < 1e-4
         assert torch.max(torch.abs(a["lufs_inst"] - c["lufs_inst"])).item() < 1e-3
