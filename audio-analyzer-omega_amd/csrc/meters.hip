@@ -42,73 +42,97 @@ __device__ __forceinline__ float unkey(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
 
-// number of entries of a[0..n) (sorted ascending, distinct) that are < v
-__device__ __forceinline__ int lower_rank(const unsigned long long* a, int n, unsigned long long v) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (a[mid] < v)
-      lo = mid + 1;
-    else
-      hi = mid;
+// For each of Q values v[q]: the number of entries of a[0..n) (sorted ascending, distinct) below it.
+// Fixed-step (branch-free) binary searches, interleaved so the Q dependent LDS chains overlap.
+template <int Q>
+__device__ __forceinline__ void lower_ranks(const unsigned long long* a, int n, const unsigned long long (&v)[Q],
+                                            int (&r)[Q]) {
+#pragma unroll
+  for (int q = 0; q < Q; ++q) r[q] = 0;
+  if (n <= 0) return;
+  for (int step = 1 << (31 - __builtin_clz(n)); step > 0; step >>= 1) {
+    // unconditional (clamped) loads: all Q issue before the first wait
+    unsigned long long e[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) e[q] = a[min(r[q] + step, n) - 1];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) r[q] += (r[q] + step <= n && e[q] < v[q]) ? step : 0;
   }
-  return lo;
 }
 
-// exclusive block scan of one int per thread (1024 threads); returns the block total
-__device__ __forceinline__ int block_excl_scan(int v, int* wsum, int tid, int& excl) {
-  const int lane = tid & 63, wv = tid >> 6;
-  int incl = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int o = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += o;
-  }
-  if (lane == 63) wsum[wv] = incl;
-  __syncthreads();
-  int base = 0, tot = 0;
-  for (int w = 0; w < 16; ++w) {
-    base += w < wv ? wsum[w] : 0;
-    tot += wsum[w];
-  }
-  __syncthreads();
-  excl = base + incl - v;
-  return tot;
+// ---- wave / block prefix sums without address registers: DPP row shifts (rows of 16 lanes, zero
+// fill), a ds_swizzle broadcast of lane 15 within each 32-lane half, readlane 31 ----
+template <int D>
+__device__ __forceinline__ int row_shr_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x110 + D, 0xF, 0xF, true); }
+__device__ __forceinline__ int bcast15_i(int v) { return __builtin_amdgcn_ds_swizzle(v, 0 | (15 << 5)); }
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+  v += row_shr_i<1>(v);
+  v += row_shr_i<2>(v);
+  v += row_shr_i<4>(v);
+  v += row_shr_i<8>(v);
+  const int h = bcast15_i(v);
+  v += (lane & 16) ? h : 0;
+  const int w = __builtin_amdgcn_readlane(v, 31);
+  return v + (lane >= 32 ? w : 0);
+}
+__device__ __forceinline__ double wave_incl_scan(double v, int lane) {
+  auto sh = [](double x, auto op) {
+    const long long b = __double_as_longlong(x);
+    const int lo = op((int)(b & 0xFFFFFFFFll)), hi = op((int)(b >> 32));
+    return __hiloint2double(hi, lo);
+  };
+  v += sh(v, [](int x) { return row_shr_i<1>(x); });
+  v += sh(v, [](int x) { return row_shr_i<2>(x); });
+  v += sh(v, [](int x) { return row_shr_i<4>(x); });
+  v += sh(v, [](int x) { return row_shr_i<8>(x); });
+  const double h = sh(v, [](int x) { return bcast15_i(x); });
+  v += (lane & 16) ? h : 0.0;
+  const double w = sh(v, [](int x) { return __builtin_amdgcn_readlane(x, 31); });
+  return v + (lane >= 32 ? w : 0.0);
 }
 
-// two exclusive int scans and one double scan in one pass (1024 threads)
-__device__ __forceinline__ void block_excl_scan3(int a, int b, double d, int* wsa, int* wsb, double* wsd, int tid,
-                                                 int& ea, int& eb, double& ed) {
+// Exclusive block scans (1024 threads) of three ints and one double in one pass; tot* = block totals.
+// ws*: 16-entry LDS scratch each (reusable after return).
+struct Scan4 {
+  int a, b, c;
+  double d;
+};
+__device__ __forceinline__ Scan4 block_excl_scan4(const Scan4& x, int* wsa, int* wsb, int* wsc, double* wsd, int tid,
+                                                  Scan4& tot) {
   const int lane = tid & 63, wv = tid >> 6;
-  int ia = a, ib = b;
-  double id = d;
-#pragma unroll
-  for (int s = 1; s < 64; s <<= 1) {
-    const int oa = __shfl_up(ia, s, 64), ob = __shfl_up(ib, s, 64);
-    const double od = __shfl_up(id, s, 64);
-    if (lane >= s) {
-      ia += oa;
-      ib += ob;
-      id += od;
-    }
-  }
+  const int ia = wave_incl_scan(x.a, lane), ib = wave_incl_scan(x.b, lane), ic = wave_incl_scan(x.c, lane);
+  const double id = wave_incl_scan(x.d, lane);
   if (lane == 63) {
     wsa[wv] = ia;
     wsb[wv] = ib;
+    wsc[wv] = ic;
     wsd[wv] = id;
   }
   __syncthreads();
-  int ba = 0, bb = 0;
-  double bd = 0.0;
-  for (int w = 0; w < wv; ++w) {
-    ba += wsa[w];
-    bb += wsb[w];
-    bd += wsd[w];
-  }
+  // the 16 wave totals, scanned by every wave; wave wv takes the prefix of waves < wv
+  const bool in = lane < 16;
+  const int sa = wave_incl_scan(in ? wsa[lane & 15] : 0, lane), sb = wave_incl_scan(in ? wsb[lane & 15] : 0, lane),
+            sc = wave_incl_scan(in ? wsc[lane & 15] : 0, lane);
+  const double sd = wave_incl_scan(in ? wsd[lane & 15] : 0.0, lane);
   __syncthreads();
-  ea = ba + ia - a;
-  eb = bb + ib - b;
-  ed = bd + id - d;
+  const int pw = wv > 0 ? wv - 1 : 0;
+  auto rl = [&](int v) { return wv > 0 ? __builtin_amdgcn_readlane(v, pw) : 0; };
+  auto rld = [&](double v) {
+    const long long b = __double_as_longlong(v);
+    return wv > 0 ? __hiloint2double(__builtin_amdgcn_readlane((int)(b >> 32), pw),
+                                     __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFFll), pw))
+                  : 0.0;
+  };
+  tot.a = __builtin_amdgcn_readlane(sa, 15);
+  tot.b = __builtin_amdgcn_readlane(sb, 15);
+  tot.c = __builtin_amdgcn_readlane(sc, 15);
+  {
+    const long long b = __double_as_longlong(sd);
+    tot.d = __hiloint2double(__builtin_amdgcn_readlane((int)(b >> 32), 15),
+                             __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFFll), 15));
+  }
+  return Scan4{rl(sa) + ia - x.a, rl(sb) + ib - x.b, rl(sc) + ic - x.c, rld(sd) + id - x.d};
 }
 
 // Window of batch frame f as absolute frame indices [lo, hi] (hi = T0 + f).
@@ -125,9 +149,12 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   __shared__ unsigned long long U[kSeqCap];   // A merged with B
   __shared__ float V[kSeqCap];                // time-ordered LUFS_inst, history ++ batch
   __shared__ int kp[kHistCap];                // exclusive prefix of kept flags over A (key order)
-  __shared__ int kb[kNewCap];                 // exclusive prefix of kept flags over B (key order)
-  __shared__ int wsa[16], wsb[16];
+  // exclusive prefix of kept flags over B (key order); before that (rank sort) the batch's 64-bit
+  // keys in time order (~0ull: not gated)
+  __shared__ __attribute__((aligned(16))) int kb[kNewCap];
+  __shared__ int wsa[16], wsb[16], wsc[16];
   __shared__ double wsd[16];
+  unsigned long long* K64 = reinterpret_cast<unsigned long long*>(kb);
   const int c = blockIdx.x, tid = threadIdx.x;
   const int C = p.C, F = (int)p.n_frames;
   const uint32_t T0 = p.t0_in[c];
@@ -136,12 +163,20 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   const int64_t thr = (int64_t)T0 + F - p.HL;  // oldest absolute index the next batch's windows reach
   const float gate = p.gate;
   OMEGA_STAMP(0);
-  // 1) stage the sequence and the sorted history (loads of a thread issued together)
+  // 1) stage the sequence and the sorted history (loads of a thread issued together); the batch's
+  // value keys for the rank sort
 #pragma unroll
   for (int q = 0; q < kSeqCap / 1024; ++q) {
     const int u = q * 1024 + tid;
-    if (u < L) V[u] = u < nh ? p.hist_l_in[(int64_t)c * p.HL + u] : p.lufs[(int64_t)(u - nh) * C + c];
+    if (u < L) {
+      const float v = u < nh ? p.hist_l_in[(int64_t)c * p.HL + u] : p.lufs[(int64_t)(u - nh) * C + c];
+      V[u] = v;
+      if (u >= nh && F <= 1024)
+        K64[u - nh] = v > gate ? ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)(u - nh))
+                               : ~0ull;
+    }
   }
+  if (F <= 1024 && tid == 0) K64[F] = ~0ull;  // padding of the last 16-byte read
 #pragma unroll
   for (int q = 0; q < kHistCap / 1024; ++q) {
     const int i = q * 1024 + tid;
@@ -149,31 +184,34 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   }
   __syncthreads();
   OMEGA_STAMP(1);
-  auto bkey = [&](int f) -> unsigned long long {
-    const float v = V[nh + f];
-    return v > gate ? ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)f) : ~0ull;
-  };
   // 2) sort the batch's gated keys (distinct: they carry the frame index). Up to 1024 frames: rank
-  // sort, P threads per key (adjacent lanes) each counting the smaller keys of a 1/P slice; beyond:
-  // bitonic.
+  // sort, P threads per key (adjacent lanes) each counting the smaller keys of a 1/P slice (16-byte
+  // reads); beyond: bitonic.
   int Gn;
   int Fp = 1;
   while (Fp < F) Fp <<= 1;
   if (Fp <= 1024) {
     const int P = min(64, 1024 / Fp);
     const int f = tid / P, part = tid % P;
-    const int len = (F + P - 1) / P, g0 = part * len, g1 = min(F, g0 + len);
-    const unsigned long long k = f < F ? bkey(f) : ~0ull;
+    const int len = (((F + P - 1) / P) + 1) & ~1, g0 = part * len, g1 = min(F, g0 + len);
+    const unsigned long long kf = f < F ? K64[f] : ~0ull;
     int rank = 0;
-    if (k != ~0ull) {
+    if (kf != ~0ull) {
 #pragma unroll 8
-      for (int g = g0; g < g1; ++g) rank += bkey(g) < k;
+      for (int g = g0; g < g1; g += 2) {
+        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(K64 + g);
+        rank += q.x < kf;
+        rank += q.y < kf;
+      }
     }
     for (int o = 1; o < P; o <<= 1) rank += __shfl_xor(rank, o, 64);
-    int dummy;
-    Gn = block_excl_scan(part == 0 && k != ~0ull ? 1 : 0, wsa, tid, dummy);
-    if (part == 0 && k != ~0ull) B[rank] = k;
+    Gn = __syncthreads_count(part == 0 && kf != ~0ull);
+    if (part == 0 && kf != ~0ull) B[rank] = kf;
   } else {
+    auto bkey = [&](int f) -> unsigned long long {
+      const float v = V[nh + f];
+      return v > gate ? ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)f) : ~0ull;
+    };
     for (int f = tid; f < Fp; f += 1024) B[f] = f < F ? bkey(f) : ~0ull;
     __syncthreads();
     for (int k = 2; k <= Fp; k <<= 1) {
@@ -193,9 +231,11 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     }
     int gn_part = 0;
     for (int i = tid; i < Fp; i += 1024) gn_part += B[i] != ~0ull;
-    int dummy;
-    Gn = block_excl_scan(gn_part, wsa, tid, dummy);
+    Scan4 tot;
+    block_excl_scan4(Scan4{gn_part, 0, 0, 0.0}, wsa, wsb, wsc, wsd, tid, tot);
+    Gn = tot.a;
   }
+  __syncthreads();  // B complete; K64 (kb) free for the kept prefixes
   OMEGA_STAMP(2);
   // 3) kept flags (absolute index >= thr) and their key-order prefixes, for A and B
   constexpr int PA = kHistCap / 1024, PB = kNewCap / 1024;
@@ -214,9 +254,9 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
       fb[q] = i < Gn && (int64_t)(uint32_t)B[i] >= thr;
       sb += fb[q];
     }
-    int ea, eb;
-    double ed;
-    block_excl_scan3(sa, sb, 0.0, wsa, wsb, wsd, tid, ea, eb, ed);
+    Scan4 tot;
+    const Scan4 e = block_excl_scan4(Scan4{sa, sb, 0, 0.0}, wsa, wsb, wsc, wsd, tid, tot);
+    int ea = e.a, eb = e.b;
 #pragma unroll
     for (int q = 0; q < PA; ++q) {
       kp[tid * PA + q] = ea;
@@ -227,26 +267,42 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
       kb[tid * PB + q] = eb;
       eb += fb[q];
     }
-    if (tid == 1023) {
-      wsa[0] = ea;  // totals, read after the barrier below
-      wsb[0] = eb;
-    }
+    Ka = tot.a;
+    Kb = tot.b;
   }
   __syncthreads();
-  Ka = wsa[0];
-  Kb = wsb[0];
   OMEGA_STAMP(3);
   // 4) the merged list U, and the next sorted history (kept ones), by rank
   unsigned long long* S = p.skeys_out + (int64_t)c * p.HL;
-  for (int i = tid; i < ns; i += 1024) {
-    const int r = lower_rank(B, Gn, A[i]);
-    U[i + r] = A[i];
-    if ((int64_t)(uint32_t)A[i] >= thr) S[kp[i] + (r < Gn ? kb[r] : Kb)] = A[i];
+  {
+    unsigned long long av[PA];
+    int ra[PA];
+#pragma unroll
+    for (int q = 0; q < PA; ++q) av[q] = q * 1024 + tid < ns ? A[q * 1024 + tid] : ~0ull;
+    lower_ranks<PA>(B, Gn, av, ra);
+#pragma unroll
+    for (int q = 0; q < PA; ++q) {
+      const int i = q * 1024 + tid, r = ra[q];
+      if (i < ns) {
+        U[i + r] = av[q];
+        if ((int64_t)(uint32_t)av[q] >= thr) S[kp[i] + (r < Gn ? kb[r] : Kb)] = av[q];
+      }
+    }
   }
-  for (int j = tid; j < Gn; j += 1024) {
-    const int r = lower_rank(A, ns, B[j]);
-    U[j + r] = B[j];
-    if ((int64_t)(uint32_t)B[j] >= thr) S[kb[j] + (r < ns ? kp[r] : Ka)] = B[j];
+  {
+    unsigned long long bv[PB];
+    int rb[PB];
+#pragma unroll
+    for (int q = 0; q < PB; ++q) bv[q] = q * 1024 + tid < Gn ? B[q * 1024 + tid] : ~0ull;
+    lower_ranks<PB>(A, ns, bv, rb);
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int j = q * 1024 + tid, r = rb[q];
+      if (j < Gn) {
+        U[j + r] = bv[q];
+        if ((int64_t)(uint32_t)bv[q] >= thr) S[kb[j] + (r < ns ? kp[r] : Ka)] = bv[q];
+      }
+    }
   }
   __syncthreads();
   OMEGA_STAMP(4);
@@ -275,12 +331,10 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
       gd += (double)V[u];
     }
   }
-  int ec, ee;
-  double ed;
-  block_excl_scan3(cc, ce, gd, wsa, wsb, wsd, tid, ec, ee, ed);
-  int eg, dummy_b;
-  double dummy_d;
-  block_excl_scan3(gi, 0, 0.0, wsa, wsb, wsd, tid, eg, dummy_b, dummy_d);
+  Scan4 tot;
+  const Scan4 ex = block_excl_scan4(Scan4{cc, ce, gi, gd}, wsa, wsb, wsc, wsd, tid, tot);
+  int ec = ex.a, ee = ex.b, eg = ex.c;
+  double ed = ex.d;
   OMEGA_STAMP(5);
   float* core = p.core + (int64_t)c * kSeqCap;
   MeterExt* ext = p.ext + (int64_t)c * kSeqCap;
