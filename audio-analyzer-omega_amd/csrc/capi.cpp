@@ -27,6 +27,7 @@ hipError_t launch_mrfft(const SpectralParams& p, hipStream_t s);
 hipError_t launch_mrfft_range(const SpectralParams& p, int r0, int r1, hipStream_t s);
 hipError_t launch_mrfft_independent(const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
+hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
 hipError_t launch_spectra(int m, const SpectraParams& p, int grid, hipStream_t s);
@@ -191,6 +192,8 @@ struct omega_ctx {
   int64_t tpx_cap = 0;
   bool tp_l2 = false;       // 512-thread true peak with the spectrum in L2 (OMEGA_TP_L2=1; measured slower)
   bool fuse_frame = false;  // W = 16384: K-weighting + true peak in one kernel (OMEGA_FUSE=1 enables)
+  int rf_sizes = 1 << 14;   // resolution sizes on the register-FFT kernel (OMEGA_RF_SIZES bit mask)
+  bool tp_rf = true;        // register-FFT true peak for W = 8192 / 16384 (OMEGA_TP_RF=0: the LDS-pass kernel)
   std::map<std::pair<int, int>, float*> windows;  // (m, kind) -> device window
   std::map<int, float2*> rots;                     // m -> true-peak rotation table
   // combine plan as per-target owner lists (CSR) for omega_combine over a subset of resolutions
@@ -389,6 +392,13 @@ void drop_graphs(omega_ctx* c) {
   c->graphs.clear();
 }
 
+// True-peak kernel choice: the register-FFT kernel for 8192- and 16384-sample frames (unless
+// OMEGA_TP_RF=0 or the L2-scratch variant is selected), otherwise the LDS-pass kernel.
+hipError_t tp_launch(omega_ctx* c, int W, const SpectralParams& sp, hipStream_t s) {
+  if (c->tp_rf && !sp.tp_scratch && (W == 16384 || W == 8192)) return launch_truepeak_rf(W, sp, s);
+  return launch_truepeak(W, sp, s);
+}
+
 // Spectrum scratch of the 512-thread true-peak kernel (W = 16384): 64 KiB per channel-frame, grown
 // on demand up to 8192 channel-frames (larger calls use the register-resident kernel). Growing
 // drops the captured graphs, which hold the old pointer.
@@ -564,6 +574,7 @@ SpectralParams spectral_params(omega_ctx* c) {
   SpectralParams p{};
   p.C = c->cfg.n_channels;
   p.n_res = c->cfg.n_res;
+  p.rf_sizes = c->rf_sizes;
   for (int r = 0; r < p.n_res; ++r) {
     ResParam& q = p.res[r];
     q.n = c->cfg.res[r].fft_size;
@@ -696,7 +707,7 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
                       sp.res[3].mag_out;
   if (c->layout == 0) {
     if (do_res) HIPC(c, c->res_independent ? launch_mrfft_independent(sp, s) : launch_mrfft(sp, s));
-    if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
+    if (do_tp) HIPC(c, tp_launch(c, W, sp, s));
     if (do_kw) HIPC(c, launch_kweight(W, kp, s));
     return meters ? meters_enqueue(c, lufs, tp, n_frames, meters, s, nullptr) : 0;
   }
@@ -736,7 +747,7 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
       HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
     }
     if (do_res) HIPC(c, c->res_independent ? launch_mrfft_independent(sp, s) : launch_mrfft(sp, s));
-    if (do_tp) HIPC(c, launch_truepeak(W, sp, s));
+    if (do_tp) HIPC(c, tp_launch(c, W, sp, s));
     for (MeterPrepParams p : mc) {
       p.parts = 2;
       HIPC(c, launch_meter_query(p, s));
@@ -746,7 +757,7 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
   }
   if (do_tp) {
     HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_fork, 0));
-    HIPC(c, launch_truepeak(W, sp, c->fork[1]));
+    HIPC(c, tp_launch(c, W, sp, c->fork[1]));
     HIPC(c, hipEventRecord(c->ev_join[1], c->fork[1]));
   }
   if (do_res) {
@@ -813,6 +824,8 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   c->stream = c->own;
   if (const char* fz = std::getenv("OMEGA_FUSE")) c->fuse_frame = std::atoi(fz) != 0;
   if (const char* tl = std::getenv("OMEGA_TP_L2")) c->tp_l2 = std::atoi(tl) != 0;
+  if (const char* tr = std::getenv("OMEGA_TP_RF")) c->tp_rf = std::atoi(tr) != 0;
+  if (const char* rs = std::getenv("OMEGA_RF_SIZES")) c->rf_sizes = std::atoi(rs) & ((1 << 14) | (1 << 13));
   if (const char* gr = std::getenv("OMEGA_GRAPHS")) c->use_graph = std::atoi(gr) != 0;
   if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
     const int v = std::atoi(lay);
@@ -1081,7 +1094,7 @@ int omega_true_peak(omega_ctx* c, const float* x, int64_t n, int32_t m, float* o
   if (!e) e = tp_scratch(c, m, n, &sp.tp_scratch);
   if (e) return e;
   sp.rot = rot;
-  HIPC(c, launch_spectral(m, sp, c->stream));
+  HIPC(c, tp_launch(c, m, sp, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 }

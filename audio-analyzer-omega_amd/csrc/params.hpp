@@ -44,6 +44,7 @@ struct SpectralParams {
   const float2* rot;  // [W/2 + 1] exp(+2 pi i k / (4W))
   float4* tp_scratch;  // [n_cf, W/4] half-spectrum pairs of the 512-thread true-peak kernel (L2-resident)
   const float2* tw[kMaxLog2];  // tw[l][m] = exp(-2 pi i m / 2^l)
+  int rf_sizes;  // host-side launch choice: bit log2(N) set = resolution size N runs on the register-FFT kernel
 };
 
 // One zero-phase biquad (filtfilt with scipy's defaults) in state-space form:

@@ -1,0 +1,149 @@
+// Register-resident block FFT for gfx950: K = 16 * NTH complex points, each of the NTH threads
+// holding 16 of them in VGPRs for the whole transform. Three radix-16 passes run in registers with
+// two LDS exchanges between them (instead of one LDS round trip per radix pass), so a 512-thread
+// workgroup needs 64 KiB of LDS and two workgroups (two frames) share a CU: one's LDS exchange
+// overlaps the other's butterflies. Model and bank-conflict check: tools/model/regfft_model.py.
+//
+// Decimation in frequency, K = 16 * 16 * L (L = 32 for K = 8192, L = 16 for K = 4096):
+//   pass 1, thread t:             a[r] = x[t + NTH r]   DFT16 over r -> k1, twiddle W_K^{t k1}
+//   exchange 1 -> thread (u, k1): b[v] = B_{u + L v}[k1] DFT16 over v -> k2, twiddle W_K^{16 u k2}
+//   exchange 2 -> pass 3:
+//     L = 16, thread (k2, k1):    c[u] = C_u[k2][k1]     DFT16 over u -> m
+//                                 X[k1 + 16 k2 + 256 m]
+//     L = 32, thread (q, k2, k1), q = lane bit 0: c[u'] = C_{q + 2u'} DFT16 over u' -> m, odd lanes
+//                                 times w32^m, butterfly with the neighbour lane (DPP)
+//                                 X[k1 + 16 k2 + 256 (m + 16 q)]
+// LDS slots are XOR-swizzled so every exchange is free of bank conflicts (ds_write_b64 groups of
+// 16 lanes, ds_read_b64 groups of 32); the natural-order slot map a3 (for consumers that read the
+// spectrum by frequency: untangles, magnitudes) costs at most one extra cycle on mirror reads.
+#pragma once
+#include "fft.hpp"
+
+namespace omega {
+
+// cos / sin(2 pi r / 128), r < 16: the true-peak rotation e^{2 pi i k / 4M} of element
+// k = t + NTH r relative to the thread's base k = t (NTH / 4M = 1/128 for M = 32 NTH)
+__device__ constexpr float kCos128[16] = {
+    1.000000000e+00f, 9.987954562e-01f, 9.951847267e-01f, 9.891765100e-01f, 9.807852804e-01f,
+    9.700312532e-01f, 9.569403357e-01f, 9.415440652e-01f, 9.238795325e-01f, 9.039892931e-01f,
+    8.819212643e-01f, 8.577286100e-01f, 8.314696123e-01f, 8.032075315e-01f, 7.730104534e-01f,
+    7.409511254e-01f};
+__device__ constexpr float kSin128[16] = {
+    0.000000000e+00f, 4.906767433e-02f, 9.801714033e-02f, 1.467304745e-01f, 1.950903220e-01f,
+    2.429801799e-01f, 2.902846773e-01f, 3.368898534e-01f, 3.826834324e-01f, 4.275550934e-01f,
+    4.713967368e-01f, 5.141027442e-01f, 5.555702330e-01f, 5.956993045e-01f, 6.343932842e-01f,
+    6.715589548e-01f};
+
+// lane l reads lane l ^ 1 (DPP quad_perm [1,0,3,2])
+__device__ __forceinline__ float lane_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+}
+
+template <int K>
+struct RegFFT {
+  static_assert(K == 8192 || K == 4096, "register FFT plans: K = 4096, 8192");
+  static constexpr int NTH = K / 16;
+  static constexpr int L = K / 256;
+  // LDS layouts (float2 slots), padded so that every slot is a per-thread base plus a compile-time
+  // offset per register (ds_read/ds_write immediate offsets: no per-element address arithmetic):
+  //   exchange 1, element (t, k1):       P1 k1 + t
+  //   exchange 2, element (u, k2, k1):   P2R k1 + P2C k2 + u
+  //   spectrum, frequency n:             a3(n) = n + n/16 (+ 8 for n >= 4096 when K = 8192)
+  static constexpr int P1 = L == 32 ? 512 : 272;
+  static constexpr int P2R = L == 32 ? 544 : 272;
+  static constexpr int P2C = L == 32 ? 34 : 17;
+  static constexpr int kSlots = K == 8192 ? 8712 : 4352;  // LDS buffer size in float2
+
+  static __device__ __forceinline__ int a3(int n) {
+    if constexpr (K == 8192) return n + (n >> 4) + ((n >> 12) << 3);
+    else return n + (n >> 4);
+  }
+  // bins k = t + NTH r: a3(k) = s3(t) + o3(r)
+  static __device__ __forceinline__ int s3(int t) { return t + (t >> 4); }
+  static constexpr int o3(int r) { return K == 8192 ? 544 * r + 8 * (r >> 3) : 272 * r; }
+  // mirror bins K - t - NTH r, t >= 1: s3m(t) + o3(15 - r) (K = 8192, t = 0: exact except r = 0, 8)
+  static __device__ __forceinline__ int s3m(int t) { return (NTH - t) + ((NTH - t) >> 4); }
+  // pass-3 output register m of thread s: frequency out_index(s, m), slot s3o(s) + 272 m
+  static __device__ __forceinline__ int out_index(int s, int m) {
+    if constexpr (L == 32) return (s >> 5) + 16 * ((s >> 1) & 15) + 256 * (m + 16 * (s & 1));
+    else return (s >> 4) + 16 * (s & 15) + 256 * m;
+  }
+  static __device__ __forceinline__ int s3o(int s) {
+    if constexpr (L == 32) return (s >> 5) + 17 * ((s >> 1) & 15) + 4360 * (s & 1);
+    else return (s >> 4) + 17 * (s & 15);
+  }
+
+  // v[k] *= w^k, k = 1..15 (powers by a multiply chain)
+  static __device__ __forceinline__ void twiddle(float2 (&v)[16], float2 w) {
+    float2 wk = w;
+    static_for<1, 16>([&](auto k) {
+      v[k] = cmul(v[k], wk);
+      if constexpr (k + 1 < 16) wk = cmul(wk, w);
+    });
+  }
+
+  // 16-point DFT in registers, natural order out
+  static __device__ __forceinline__ void dft16(float2 (&v)[16]) {
+    dft_dif<16>(v);
+    float2 o[16];
+    static_for<0, 16>([&](auto m) { o[m] = v[brev<16>(m)]; });
+    static_for<0, 16>([&](auto m) { v[m] = o[m]; });
+  }
+
+  // Forward FFT. In: v[r] = x[t + NTH r]. Out: v[m] = X[out_index(t, m)]. w1 = W_K^t and
+  // w2 = W_K^{16 (t mod L)} (the thread's twiddle bases, loaded once per kernel). SYNC: `buf` may
+  // still be read by other threads on entry -- a barrier precedes the first exchange write (after
+  // pass 1's arithmetic, so the butterflies overlap the stragglers' reads).
+  template <bool SYNC = false>
+  static __device__ __forceinline__ void run(float2 (&v)[16], float2* buf, int t, float2 w1, float2 w2) {
+    // pass 1
+    dft16(v);
+    twiddle(v, w1);
+    if constexpr (SYNC) __syncthreads();
+    {
+      float2* b = buf + t;
+      static_for<0, 16>([&](auto k1) { b[P1 * k1] = v[k1]; });
+    }
+    __syncthreads();
+    // pass 2
+    {
+      const int u = t % L, k1 = t / L;
+      const float2* b = buf + P1 * k1 + u;
+      static_for<0, 16>([&](auto r) { v[r] = b[L * r]; });
+      dft16(v);
+      twiddle(v, w2);
+      __syncthreads();  // every exchange-1 read is done
+      float2* bw = buf + P2R * k1 + u;
+      static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
+    }
+    __syncthreads();
+    // pass 3
+    if constexpr (L == 16) {
+      const int k2 = t & 15, k1 = t >> 4;
+      const float2* b = buf + P2R * k1 + P2C * k2;
+      static_for<0, 16>([&](auto r) { v[r] = b[r]; });
+      dft16(v);
+    } else {
+      const int q = t & 1, k2 = (t >> 1) & 15, k1 = t >> 5;
+      const float2* b = buf + P2R * k1 + P2C * k2 + q;
+      static_for<0, 16>([&](auto r) { v[r] = b[2 * r]; });
+      dft16(v);
+      // odd lanes: F1[m] * w32^m; then out = F0 + F1' (even lane), F0 - F1' (odd lane)
+      if (q) static_for<1, 16>([&](auto m) { v[m] = twc<m, 32>(v[m]); });
+      const float s = q ? -1.f : 1.f;
+      static_for<0, 16>([&](auto m) {
+        const float px = lane_xor1(v[m].x), py = lane_xor1(v[m].y);
+        v[m] = make_float2(fmaf(v[m].x, s, px), fmaf(v[m].y, s, py));
+      });
+    }
+  }
+
+  // Natural-order spectrum exchange after run(): every register to its frequency's slot
+  // (the caller synchronises before, if the buffer may still be read, and after).
+  static __device__ __forceinline__ void store_spectrum(const float2 (&v)[16], float2* buf, int t) {
+    float2* b = buf + s3o(t);
+    static_for<0, 16>([&](auto m) { b[272 * m] = v[m]; });
+  }
+};
+
+}  // namespace omega

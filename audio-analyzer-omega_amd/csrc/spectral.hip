@@ -149,10 +149,17 @@ __global__ __launch_bounds__(256) void combine_kernel(CombineParams p) {
 
 // Resolution kernels for resolutions in [r0, r1), in resolution order (the combine owner protocol
 // relies on it whenever a target bin has several owners).
+hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s);
+
 hipError_t launch_mrfft_range(const SpectralParams& p, int r0, int r1, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
   for (int r = r0; r < r1 && r < p.n_res; ++r) {
     if (!p.comb_out && !p.res[r].mag_out) continue;
+    if ((p.rf_sizes >> ilog2(p.res[r].n)) & 1) {
+      const hipError_t e = launch_mrfft_rf(p.res[r].n, p, r, s);
+      if (e != hipSuccess) return e;
+      continue;
+    }
 #define OMEGA_RES(K) \
   hipLaunchKernelGGL(mrfft_kernel<K>, grid, dim3(threads_for<K>()), K * sizeof(float2), s, p, r)
     OMEGA_SWITCH_K(p.res[r].n, OMEGA_RES)
@@ -202,7 +209,7 @@ hipError_t launch_mrfft_independent(const SpectralParams& p, hipStream_t s) {
   for (int r = 0; r < p.n_res; ++r) {
     if (!p.comb_out && !p.res[r].mag_out) continue;
     const int n = p.res[r].n;
-    if (n > 8192) {
+    if (n > 8192 || ((p.rf_sizes >> ilog2(n)) & 1)) {
       const hipError_t e = launch_mrfft_range(p, r, r + 1, s);
       if (e != hipSuccess) return e;
       continue;

@@ -8,7 +8,8 @@
 
 namespace omega {
 
-__device__ __forceinline__ float cabs(float2 z) { return sqrtf(fmaf(z.x, z.x, z.y * z.y)); }
+// raw v_sqrt_f32 (1 ulp): no denormal-scaling sequence around it
+__device__ __forceinline__ float cabs(float2 z) { return __builtin_amdgcn_sqrtf(fmaf(z.x, z.x, z.y * z.y)); }
 
 // untangle of one pair (k, K-k), 0 < k < K/2: returns X[k] and X[K-k]
 __device__ __forceinline__ void untangle(float2 a, float2 b, float2 w, float2& xk, float2& xkk) {
