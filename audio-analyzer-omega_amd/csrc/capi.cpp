@@ -31,6 +31,7 @@ hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
 hipError_t launch_spectra(int m, const SpectraParams& p, int grid, hipStream_t s);
+hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s);
 hipError_t launch_frame(const SpectralParams& sp, const KWeightParams& kp, hipStream_t s);
 hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s);
@@ -193,6 +194,7 @@ struct omega_ctx {
   bool tp_l2 = false;       // 512-thread true peak with the spectrum in L2 (OMEGA_TP_L2=1; measured slower)
   bool fuse_frame = false;  // W = 16384: K-weighting + true peak in one kernel (OMEGA_FUSE=1 enables)
   int rf_sizes = 1 << 14;   // resolution sizes on the register-FFT kernel (OMEGA_RF_SIZES bit mask)
+  bool spectra_rf = true;   // register-FFT cfg3 spectra kernel for 8192-point frames (OMEGA_SPECTRA_RF=0: old)
   bool tp_rf = true;        // register-FFT true peak for W = 8192 / 16384 (OMEGA_TP_RF=0: the LDS-pass kernel)
   std::map<std::pair<int, int>, float*> windows;  // (m, kind) -> device window
   std::map<int, float2*> rots;                     // m -> true-peak rotation table
@@ -825,6 +827,7 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   if (const char* fz = std::getenv("OMEGA_FUSE")) c->fuse_frame = std::atoi(fz) != 0;
   if (const char* tl = std::getenv("OMEGA_TP_L2")) c->tp_l2 = std::atoi(tl) != 0;
   if (const char* tr = std::getenv("OMEGA_TP_RF")) c->tp_rf = std::atoi(tr) != 0;
+  if (const char* sr = std::getenv("OMEGA_SPECTRA_RF")) c->spectra_rf = std::atoi(sr) != 0;
   if (const char* rs = std::getenv("OMEGA_RF_SIZES")) c->rf_sizes = std::atoi(rs) & ((1 << 14) | (1 << 13));
   if (const char* gr = std::getenv("OMEGA_GRAPHS")) c->use_graph = std::atoi(gr) != 0;
   if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
@@ -1421,7 +1424,10 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
   p.chroma_out = dcr;
   for (int l = 0; l < kMaxLog2; ++l) p.tw[l] = c->d_tw[l];
   const int grid = (int)std::min<int64_t>(n, 2 * (int64_t)c->n_cu);
-  HIPC(c, launch_spectra(m, p, grid, c->stream));
+  if (c->spectra_rf && m == 8192)
+    HIPC(c, launch_spectra_rf(m, p, c->stream));
+  else
+    HIPC(c, launch_spectra(m, p, grid, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 }

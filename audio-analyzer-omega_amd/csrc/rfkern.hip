@@ -217,6 +217,171 @@ hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s)
   return hipGetLastError();
 }
 
+// Fused spectrum analysis (cfg3: A13 -> A10 + A12, see spectra.hip for the reference mapping) on the
+// register FFT: one 256-thread workgroup per frame of 2K samples, four workgroups per CU (36 KiB of
+// LDS each: the exchange buffer, reused for the contiguous magnitudes and the chroma partials; the
+// band and chroma tables are read from global memory, L1/L2-resident).
+constexpr int kSpecRfThreads = 256;
+constexpr int kSpecRfPeakWords = 12;  // peak bitmap of bins < 768: suppression reaches k / 2 < 1408 / 2
+
+template <int K>
+__global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraParams p) {
+  using FFT = RegFFT<K>;
+  constexpr int NTH = FFT::NTH;
+  static_assert(NTH == kSpecRfThreads, "one 256-thread workgroup per frame");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float2* buf = reinterpret_cast<float2*>(smem);
+  float* magc = reinterpret_cast<float*>(smem);  // |X_k|, k <= K, once the untangle is done
+  double* part = reinterpret_cast<double*>(smem + ((K + 1) * sizeof(float) + 15) / 16 * 16);  // [240][5]
+  static_assert(((K + 1) * sizeof(float) + 15) / 16 * 16 + 240 * 5 * sizeof(double) <= FFT::kSlots * sizeof(float2),
+                "chroma partials fit the exchange buffer");
+  __shared__ unsigned long long pkw[kSpecRfPeakWords];
+  __shared__ float redf[NTH / 64];
+  __shared__ double cls[12][5];
+  const int t = threadIdx.x;
+  const int64_t fr = blockIdx.x;
+  const float2* x2 = reinterpret_cast<const float2*>(p.x + fr * p.stride);
+  const float2* w2 = reinterpret_cast<const float2*>(p.win);
+  float2 v[16];
+  static_for<0, 16>([&](auto r) {
+    const float2 a = x2[t + NTH * r], w = w2[t + NTH * r];
+    v[r] = make_float2(a.x * w.x, a.y * w.y);
+  });
+  const float2* __restrict__ twK = p.tw[ilog2(K)];
+  const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];
+  const float2 wm = p.tw[ilog2(2 * K)][t];
+  FFT::run(v, buf, t, w1, w2b);
+  __syncthreads();
+  FFT::store_spectrum(v, buf, t);
+  __syncthreads();
+  float mg[16];
+  float mnyq = 0.f, mx = 0.f;
+  {
+    const float2* bo = buf + FFT::s3(t);
+    const float2* bm = buf + FFT::s3m(t);
+    static_for<0, 16>([&](auto q) {
+      const float2 a = bo[FFT::o3(q)];
+      const float2 b = bm[FFT::o3(15 - q)];
+      float2 xk, xkk;
+      untangle(a, b, twc<q, 32>(wm), xk, xkk);
+      mg[q] = cabs(xk);
+      if constexpr (q == 0) {
+        if (t == 0) {
+          mg[0] = fabsf(a.x + a.y);
+          mnyq = fabsf(a.x - a.y);
+        }
+      }
+      mx = fmaxf(mx, mg[q]);
+    });
+  }
+  mx = fmaxf(mx, mnyq);
+  __syncthreads();  // the untangle reads are done: the buffer becomes the magnitude array
+  static_for<0, 16>([&](auto q) { magc[t + NTH * q] = mg[q]; });
+  if (t == 0) magc[K] = mnyq;
+  const float thr = block_max<NTH>(mx, redf, t) * 0.1f;  // np.max(fft) * 0.1 in float32 (barriers publish magc)
+  if (p.mag_out) {
+    float* o = p.mag_out + fr * (K + 1);
+    static_for<0, 16>([&](auto q) { o[t + NTH * q] = mg[q]; });
+    if (t == 0) o[K] = mnyq;
+  }
+  if (p.bands_out) {
+    float* o = p.bands_out + fr * p.n_out;
+    for (int i = t; i < p.n_out; i += NTH) {
+      float val = 0.f;
+      if (i < p.n_valid) {
+        const int s = p.starts[i], e = p.ends[i];
+        if (s < K + 1 && e <= K + 1) {
+          float m0 = magc[s], m1 = m0, m2 = m0, m3 = m0;
+          int k = s + 1;
+          for (; k + 3 < e; k += 4) {
+            m0 = fmaxf(m0, magc[k]);
+            m1 = fmaxf(m1, magc[k + 1]);
+            m2 = fmaxf(m2, magc[k + 2]);
+            m3 = fmaxf(m3, magc[k + 3]);
+          }
+          for (; k < e; ++k) m0 = fmaxf(m0, magc[k]);
+          val = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)) * (p.scale ? p.scale[i] : 1.f);
+        }
+      }
+      o[i] = val;
+    }
+  }
+  if (!p.chroma_out) return;
+  // strict local maxima above 0.1 max (chromagram.py:166-170) among bins 1..K-1 below 768 (the only
+  // ones a suppressed bin k / h, k < c_hi <= 1408, can name): bin t + NTH q is lane t % 64 of wave
+  // t / 64, its neighbours in the adjacent lanes (DPP) or, at the wave edges, in LDS; one ballot per
+  // 64 bins -> word 4 q + wave
+  {
+    const int lane = t & 63, w = t >> 6;
+    static_for<0, kSpecRfPeakWords / (NTH / 64)>([&](auto q) {
+      const int k = t + NTH * q;
+      const float val = mg[q];
+      float lo = wave_shift1<true>(val), hi = wave_shift1<false>(val);
+      if (lane == 0) lo = k >= 1 ? magc[k - 1] : 0.f;
+      if (lane == 63) hi = magc[k + 1];
+      const bool pk = k >= 1 && k <= K - 1 && val > lo && val > hi && val > thr;
+      const unsigned long long m = __ballot(pk);
+      if (lane == 0) pkw[4 * q + w] = m;
+    });
+  }
+  __syncthreads();
+  auto is_peak = [&](int q) { return q < 64 * kSpecRfPeakWords && (int)((pkw[q >> 6] >> (q & 63)) & 1ull); };
+  constexpr int kGrp = 20;  // threads per base-class group (12 x 20 = 240 of 256)
+  if (t < 12 * kGrp) {
+    double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    const int g = t / kGrp, r = t % kGrp;
+    const int j0 = p.cgoff[g], j1 = p.cgoff[g + 1];
+    for (int j = j0 + r; j < j1; j += kGrp) {
+      const int i = p.cperm[j];
+      const int k = p.c_lo + i;
+      // harmonic suppression (chromagram.py:172-187) in the reference's order (descending h);
+      // float32 multiplies by float32(1/h)
+      float e = magc[k];
+      if (k % 5 == 0 && is_peak(k / 5)) e = e * (1.0f / 5.0f);
+      if (k % 4 == 0 && is_peak(k / 4)) e = e * (1.0f / 4.0f);
+      if (k % 3 == 0 && is_peak(k / 3)) e = e * (1.0f / 3.0f);
+      if (k % 2 == 0 && is_peak(k / 2)) e = e * (1.0f / 2.0f);
+      const float4 cw = p.cw4[i];
+      const double ed = (double)e;
+      acc[0] = fma(ed, (double)cw.x, acc[0]);
+      acc[1] = fma(ed, (double)cw.y, acc[1]);
+      acc[2] = fma(ed, (double)cw.z, acc[2]);
+      acc[3] = fma(ed, (double)cw.w, acc[3]);
+      acc[4] = fma(ed, (double)p.cw1[i], acc[4]);
+    }
+#pragma unroll
+    for (int o = 0; o < 5; ++o) part[t * 5 + o] = acc[o];
+  }
+  __syncthreads();
+  if (t < 60) {  // group g, offset o -> class (g + o - 2) mod 12
+    const int g = t / 5, o = t % 5;
+    double sgo = 0.0;
+#pragma unroll
+    for (int r = 0; r < kGrp; ++r) sgo += part[(g * kGrp + r) * 5 + o];
+    cls[(g + o + 10) % 12][o] = sgo;
+  }
+  __syncthreads();
+  if (t < 64) {  // class sums, 3-tap circular smoothing and normalisation in one wave
+    const int c = t % 12;
+    const double ch = cls[c][0] + cls[c][1] + cls[c][2] + cls[c][3] + cls[c][4];
+    const int cm = (c + 11) % 12, cp = (c + 1) % 12;
+    const double chm = cls[cm][0] + cls[cm][1] + cls[cm][2] + cls[cm][3] + cls[cm][4];
+    const double chp = cls[cp][0] + cls[cp][1] + cls[cp][2] + cls[cp][3] + cls[cp][4];
+    const double sm = 0.25 * chm + 0.5 * ch + 0.25 * chp;
+    double tot = 0.0;
+    for (int q = 0; q < 12; ++q) tot += __shfl(sm, q, 64);
+    if (t < 12) p.chroma_out[fr * 12 + c] = tot > 0 ? sm / tot : sm;
+  }
+}
+
+hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s) {
+  // a suppressed bin k < c_hi names bin k / h >= k / 2, which must lie in the peak bitmap
+  if (m != 8192 || (p.chroma_out && p.c_hi > 2 * 64 * kSpecRfPeakWords)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spectra_rf_kernel<4096>, dim3((unsigned)p.n), dim3(kSpecRfThreads),
+                     (RegFFT<4096>::kSlots + 8) * sizeof(float2), s, p);
+  return hipGetLastError();
+}
+
 hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
   if (W == 16384) {
