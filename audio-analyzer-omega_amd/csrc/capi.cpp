@@ -40,6 +40,7 @@ hipError_t launch_bands(const BandParams& p, hipStream_t s);
 hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int hi, const double* mat, double* out,
                          hipStream_t s);
 hipError_t launch_combine(const CombineParams& p, hipStream_t s);
+hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s);
 }  // namespace omega
 
 using namespace omega;
@@ -167,11 +168,17 @@ struct omega_ctx {
   // consecutive launches (cfg2 step 149.5 us vs 128.8 us for direct launches of the same layout)
   bool use_graph = false;
   // stream layout of the per-batch work (enqueue_frames): 0 sequential, 1 concurrent branches,
-  // 2 sequential full-chip kernels with the meter aggregates on a side stream. (A variant ordered by
-  // device flags -- prep kernel's last workgroup stores a sequence number, a one-wave gate kernel
-  // waits for it before the query -- measured 124.9 us/step vs 114.9: the gate launch costs ~5 us and
-  // hipStreamWaitValue32 runs as a spinning blit kernel that holds a CU.)
-  int layout = 2;
+  // 2 sequential full-chip kernels with the meter aggregates on a side stream, 3 (default; 16384-sample
+  // frames, direct launches) one batch_kernel launch for all per-channel-frame work, the meter prep on
+  // the side stream waiting on the batch's K-weighting count (kw_done) instead of a stream event.
+  // (A variant ordered by device flags -- prep kernel's last workgroup stores a sequence number, a
+  // one-wave gate kernel waits for it before the query -- measured 124.9 us/step vs 114.9: the gate
+  // launch costs ~5 us and hipStreamWaitValue32 runs as a spinning blit kernel that holds a CU.)
+  int layout = 3;
+  unsigned* d_kw_done = nullptr;  // batch_kernel's K-weighting workgroups count themselves in here
+  unsigned kw_issued = 0;         // K-weighting workgroups launched with the count on (wraps)
+  unsigned q_issued = 0;          // LUFS-meter query workgroups launched with the count on (d_kw_done[1])
+  int batch_order = 3;            // role order of the batch launch (enqueue_batch; OMEGA_BATCH_ORDER)
   bool res_independent = false;  // no combine target has several owners: resolution kernels commute
   hipEvent_t ev_kw = nullptr;
   struct GraphEntry {
@@ -568,7 +575,10 @@ int build_meter_state(omega_ctx* c) {
   if (!e) e = dalloc(c, &c->d_next, C);
   if (!e) e = dalloc(c, &c->d_gcount, (size_t)C * (kMeterSeqCap + 1));
   if (!e) e = dalloc(c, &c->d_gsum, (size_t)C * (kMeterSeqCap + 1));
+  if (!e) e = dalloc(c, &c->d_kw_done, 4);
   if (e) return e;
+  HIPC(c, hipMemset(c->d_kw_done, 0, 4 * sizeof(unsigned)));
+  c->kw_issued = c->q_issued = 0;
   return omega_meter_reset(c);
 }
 
@@ -695,6 +705,108 @@ int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_f
   return 0;
 }
 
+// Layout 3 applies to 16384-sample frames on direct launches (a captured graph would freeze the
+// kw_done target) when every requested stage has a 512-thread batch role: the register-FFT true peak,
+// at most one 16384-point resolution (on the register FFT), the others at most 8192 points, and
+// resolutions that commute (no combine target with several owners). *mr: the 16384-point resolution.
+bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, bool do_res, hipStream_t s,
+                    int* mr) {
+  *mr = -1;
+  if (W != 16384 || s == c->cap || c->fuse_frame || sp.tp_scratch || !c->tp_rf) return false;
+  if ((kp.lufs_out || kp.weighted_out) && kp.mode != 0) return false;
+  if (!do_res) return true;
+  if (!c->res_independent) return false;
+  for (int r = 0; r < sp.n_res; ++r) {
+    if (!sp.comb_out && !sp.res[r].mag_out) continue;
+    const int n = sp.res[r].n;
+    if (n == 16384) {
+      if (*mr >= 0 || !((sp.rf_sizes >> 14) & 1)) return false;
+      *mr = r;
+    } else if (n < 512 || n > 8192) {
+      return false;
+    }
+  }
+  return true;
+}
+
+// The default layout for 16384-sample frames (c->batch_order 3). On `s`: one batch_kernel launch
+// (BatchPlan: K-weighting and 16384-point-resolution workgroups mixed, then the true peaks, then the
+// small resolutions) and the true-peak meter. On fork[0]: the meter prep (it waits on the K-weighting
+// count, kw_done) and the LUFS meters (their workgroups count themselves in). The true-peak meter's
+// first workgroup waits for that count, so `s` completes only after fork[0]'s work: no stream events
+// anywhere (each event record / wait cost ~7-13 us of idle GPU between kernels). cfg2 step on MI355X:
+// 96.5 us (order 3); 98.0 (2: K-weighting mixed with the true peaks), 112.9 (1: all three mixed), 106.3
+// (0: K-weighting as its own kernel first; it does not spill there but mixes with nothing); the
+// side-meter layout with events 99.7. Mixing the latency-bound K-weighting scans with transform work
+// is what pays; the K-weighting body spills in the batch kernel (128 VGPRs at two workgroups per CU).
+int enqueue_batch(omega_ctx* c, const SpectralParams& sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
+                  const float* tp, double* meters, hipStream_t s, int mr, bool do_tp, bool do_kw) {
+  const int64_t n = sp.n_cf;
+  const int order = c->batch_order;
+  const bool kw_in_batch = do_kw && order != 0;
+  BatchPlan bp{};
+  int seg[2][3], ns[2] = {0, 0};
+  auto add = [&](int sg, int role, bool on) {
+    if (on) seg[sg][ns[sg]++] = role;
+  };
+  add(0, 0, kw_in_batch);
+  add(order == 1 || order == 2 ? 0 : 1, 1, do_tp);
+  add(order == 1 || order == 3 ? 0 : 1, 2, mr >= 0);
+  const int64_t groups = (n + 7) / 8;
+  int64_t end = 0;
+  for (int sg = 0; sg < 2; ++sg) {
+    bp.n_roles[sg] = ns[sg] ? ns[sg] : 1;
+    for (int i = 0; i < 3; ++i) bp.roles[sg][i] = i < ns[sg] ? seg[sg][i] : 0;
+    end += ns[sg] ? 8 * ns[sg] * groups : 0;
+    if (end > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
+    bp.seg_begin[sg + 1] = (int)end;
+  }
+  bp.mr_res = mr < 0 ? 0 : mr;
+  int64_t nwg = 0;
+  for (int r = 0; r < sp.n_res; ++r) {
+    if (r == mr || (!sp.comb_out && !sp.res[r].mag_out)) continue;
+    const int K = sp.res[r].n / 2;
+    const int G = K / 16 < 64 ? 64 : K / 16;  // threads_for<K>() for K <= 4096
+    const int fpw = 512 / G;
+    bp.multi.res[bp.multi.n_seg] = r;
+    bp.multi.wg_begin[bp.multi.n_seg] = (int)nwg;
+    ++bp.multi.n_seg;
+    nwg += (n + fpw - 1) / fpw;
+  }
+  const int64_t grid = end + nwg;
+  if (grid > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
+  std::vector<MeterPrepParams> mc;
+  if (meters) {
+    mc = meter_chunks(c, lufs, tp, n_frames, meters);
+    kp.kw_done = c->d_kw_done;
+    c->kw_issued += (unsigned)n;
+    for (size_t i = 0; i < mc.size(); ++i) {
+      MeterPrepParams p = mc[i];
+      if (i == 0) {
+        p.wait_ctr = c->d_kw_done;
+        p.wait_target = c->kw_issued;
+      }
+      HIPC(c, launch_meter_prep(p, c->fork[0]));
+      p.parts = 1;
+      p.q_done = c->d_kw_done + 1;
+      c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);
+      HIPC(c, launch_meter_query(p, c->fork[0]));
+    }
+  }
+  if (do_kw && !kw_in_batch) HIPC(c, launch_kweight(W, kp, s));
+  if (grid > 0) HIPC(c, launch_batch(sp, kp, bp, (int)grid, s));
+  for (size_t i = 0; i < mc.size(); ++i) {
+    MeterPrepParams p = mc[i];
+    p.parts = 2;
+    if (i + 1 == mc.size()) {
+      p.join_ctr = c->d_kw_done + 1;
+      p.join_target = c->q_issued;
+    }
+    HIPC(c, launch_meter_query(p, s));
+  }
+  return 0;
+}
+
 // The per-batch work (c->layout). 0 sequential: resolution kernels, true peak, K-weighting, meters on
 // `s`. 1 concurrent: true peak on fork[1] and the resolution kernels (in resolution order) on fork[0]
 // from the start; K-weighting and then the meter aggregates' prep kernel (it needs the batch's
@@ -707,7 +819,11 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
   const bool do_tp = sp.tp_out != nullptr, do_kw = kp.lufs_out || kp.weighted_out;
   const bool do_res = sp.comb_out != nullptr || sp.res[0].mag_out || sp.res[1].mag_out || sp.res[2].mag_out ||
                       sp.res[3].mag_out;
-  if (c->layout == 0) {
+  int mr = -1;
+  if (c->layout == 3 && batch_eligible(c, sp, kp, W, do_res, s, &mr))
+    return enqueue_batch(c, sp, kp, W, n_frames, lufs, tp, meters, s, mr, do_tp, do_kw);
+  const int layout = c->layout == 3 ? 2 : c->layout;
+  if (layout == 0) {
     if (do_res) HIPC(c, c->res_independent ? launch_mrfft_independent(sp, s) : launch_mrfft(sp, s));
     if (do_tp) HIPC(c, tp_launch(c, W, sp, s));
     if (do_kw) HIPC(c, launch_kweight(W, kp, s));
@@ -729,7 +845,7 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
     if (do_res) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
     return 0;
   }
-  if (c->layout == 2) {
+  if (layout == 2) {
     // the full-chip kernels back to back on `s` (K-weighting first); the meter aggregates' prep and
     // LUFS query kernels (one or two workgroups per channel: latency-bound) run on fork[0] beside the
     // resolution and true-peak kernels, the true-peak meter after the true peaks on `s`. (Concurrent
@@ -830,12 +946,22 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   if (const char* sr = std::getenv("OMEGA_SPECTRA_RF")) c->spectra_rf = std::atoi(sr) != 0;
   if (const char* rs = std::getenv("OMEGA_RF_SIZES")) c->rf_sizes = std::atoi(rs) & ((1 << 14) | (1 << 13));
   if (const char* gr = std::getenv("OMEGA_GRAPHS")) c->use_graph = std::atoi(gr) != 0;
+  if (const char* bo = std::getenv("OMEGA_BATCH_ORDER")) c->batch_order = std::atoi(bo);
   if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
     const int v = std::atoi(lay);
-    c->layout = v < 0 || v > 2 ? 2 : v;
+    c->layout = v < 0 || v > 3 ? 3 : v;
   }
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking);
-  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->fork[0], hipStreamNonBlocking);
+  if (he == hipSuccess) {
+    // fork[0] carries the latency-bound meter kernels beside full-chip work: at the highest stream
+    // priority (OMEGA_METER_PRIO=0: default priority) a freed CU goes to them first
+    int lo = 0, hi = 0;
+    const char* mp = std::getenv("OMEGA_METER_PRIO");
+    if ((!mp || std::atoi(mp) != 0) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+      he = hipStreamCreateWithPriority(&c->fork[0], hipStreamNonBlocking, hi);
+    else
+      he = hipStreamCreateWithFlags(&c->fork[0], hipStreamNonBlocking);
+  }
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->fork[1], hipStreamNonBlocking);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_join[0], hipEventDisableTiming);
@@ -884,9 +1010,10 @@ int omega_set_stream(omega_ctx* c, void* s) {
 int omega_set_graphs(omega_ctx* c, int enable) {
   if (!c) return OMEGA_EINVAL;
   c->use_graph = (enable & 1) != 0;
-  // bits 1-2: 0 default (meters on a side stream), 1 sequential, 2 concurrent branches
+  // bits 1-2: 0 default (one batch launch where eligible, else 3), 1 sequential, 2 concurrent
+  // branches, 3 full-chip kernels back to back with the meters on a side stream
   const int lay = (enable >> 1) & 3;
-  c->layout = lay == 1 ? 0 : (lay == 2 ? 1 : 2);
+  c->layout = lay == 1 ? 0 : (lay == 2 ? 1 : (lay == 3 ? 2 : 3));
   drop_graphs(c);
   return 0;
 }

@@ -230,10 +230,29 @@ __device__ __forceinline__ void gather_edges(const float (&u)[L], float* e, int 
   });
 }
 
+// LUFS_inst store of thread 0. PUB: write-through (sc1) agent-scope store, so that a counter add
+// after this thread's vmcnt drain publishes it to a consumer on another CU / XCD (batch_kernel).
+template <bool PUB>
+__device__ __forceinline__ void put_lufs(float* o, int64_t cf, float v) {
+  if constexpr (PUB)
+    __hip_atomic_store(reinterpret_cast<unsigned*>(o + cf), __float_as_uint(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else
+    o[cf] = v;
+}
+
+// After kweight_body<..., PUB = true>: thread 0 stored the value write-through; drain, then count in.
+__device__ __forceinline__ void kw_count_in(const KWeightParams& p, int tid) {
+  if (p.kw_done && tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(p.kw_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // K-weighting of channel-frame cf by a workgroup of NTH threads (all of them), chunk L = M / NTH
 // (the host tables must be built for that L). LDS from the caller: pwl[2][64] scan powers, fbuf[M]
 // parking for f (element-major), sh[4 * NW], edge[20], red[NW].
-template <int M, int NTH>
+template <int M, int NTH, bool PUB = false>
 __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf, int tid, float4 (*pwl)[64], float* fbuf,
                                              float* sh, float* edge, double* red) {
   constexpr int L = M / NTH;
@@ -270,12 +289,13 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
   float* wout = p.weighted_out ? p.weighted_out + cf * M + tid * L : nullptr;
   if (p.mode == 3) {  // Z-weighting: the signal itself, no gate
     if (wout) static_for<0, L>([&](auto i) { wout[i] = u[i]; });
-    if (tid == 0 && p.lufs_out) p.lufs_out[cf] = ms_in > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms_in)) : -100.0f;
+    if (tid == 0 && p.lufs_out)
+      put_lufs<PUB>(p.lufs_out, cf, ms_in > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms_in)) : -100.0f);
     return;
   }
   if (sqrt(ms_in) < 1e-6) {  // professional_meters.py:132-134
     if (wout) static_for<0, L>([&](auto i) { wout[i] = 0.f; });
-    if (tid == 0 && p.lufs_out) p.lufs_out[cf] = -100.0f;
+    if (tid == 0 && p.lufs_out) put_lufs<PUB>(p.lufs_out, cf, -100.0f);
     return;
   }
   gather_edges<L, NTH>(u, edge, tid);
@@ -306,7 +326,7 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
     }
   }
   const double ms = block_sum_f<NTH>(acc, red, tid) / M;
-  if (tid == 0 && p.lufs_out) p.lufs_out[cf] = ms > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms)) : -100.0f;
+  if (tid == 0 && p.lufs_out) put_lufs<PUB>(p.lufs_out, cf, ms > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms)) : -100.0f);
   OMEGA_STAMP(26);
 }
 

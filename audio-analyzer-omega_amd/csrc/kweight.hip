@@ -36,7 +36,9 @@ namespace omega {
 #endif
 constexpr int kw_waves_per_eu(int nth) { return OMEGA_KW_WG_PER_CU * nth / 256 > 0 ? OMEGA_KW_WG_PER_CU * nth / 256 : 1; }
 
-template <int M, int NTH = kw_threads(M)>
+// PUB: the LUFS value is published for a consumer on another stream (KWeightParams::kw_done); a
+// separate instantiation, so the plain kernel keeps its register allocation
+template <int M, bool PUB = false, int NTH = kw_threads(M)>
 __global__ __launch_bounds__(NTH, kw_waves_per_eu(NTH)) void kweight_kernel(KWeightParams p) {
   constexpr int NW = NTH / 64;
   static_assert(M / NTH == kw_chunk(M), "chunk length must match the host tables");
@@ -45,7 +47,8 @@ __global__ __launch_bounds__(NTH, kw_waves_per_eu(NTH)) void kweight_kernel(KWei
   __shared__ float sh[4 * NW];
   __shared__ float edge[20];
   __shared__ double red[NW];
-  kweight_body<M, NTH>(p, blockIdx.x, threadIdx.x, pwl, fbuf, sh, edge, red);
+  kweight_body<M, NTH, PUB>(p, blockIdx.x, threadIdx.x, pwl, fbuf, sh, edge, red);
+  if constexpr (PUB) kw_count_in(p, threadIdx.x);
 }
 
 OMEGA_STAMPS_GETTER(omega_debug_kw_stamps)
@@ -54,7 +57,12 @@ hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
   switch (m) {
 #define OMEGA_KW(M) \
-  case M: hipLaunchKernelGGL(kweight_kernel<M>, grid, dim3(kw_threads(M)), 0, s, p); break;
+  case M:                                                                                    \
+    if (p.kw_done)                                                                           \
+      hipLaunchKernelGGL((kweight_kernel<M, true>), grid, dim3(kw_threads(M)), 0, s, p);     \
+    else                                                                                     \
+      hipLaunchKernelGGL((kweight_kernel<M, false>), grid, dim3(kw_threads(M)), 0, s, p);    \
+    break;
     OMEGA_KW(512)
     OMEGA_KW(1024)
     OMEGA_KW(2048)

@@ -156,6 +156,19 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   __shared__ double wsd[16];
   unsigned long long* K64 = reinterpret_cast<unsigned long long*>(kb);
   const int c = blockIdx.x, tid = threadIdx.x;
+  if (p.wait_ctr) {
+    // the batch's LUFS_inst values come from batch_kernel on another stream: one lane polls the count
+    // (relaxed, bounded), then ONE agent-scope acquire before any wave reads them
+    if (tid == 0) {
+      for (int i = 0; i < (1 << 22); ++i) {
+        if ((int)(__hip_atomic_load(p.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - p.wait_target) >= 0) break;
+        __builtin_amdgcn_s_sleep(4);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
   const int C = p.C, F = (int)p.n_frames;
   const uint32_t T0 = p.t0_in[c];
   const int nh = p.n_l_in[c], ns = p.n_s_in[c];
@@ -403,7 +416,7 @@ __device__ __forceinline__ float seq_at(const float* hist, const float* batch, i
 // One wave per output (f, c); workgroup (0, c) also rolls the channel's true-peak history. parts
 // selects the LUFS meters (they need the prep kernel's output) and/or the true-peak meter (it needs the
 // batch's true peaks only), so the two can run on different streams.
-__global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
+__device__ __forceinline__ void meter_query_body(const MeterPrepParams& p) {
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.y;
   const int C = p.C;
@@ -503,6 +516,29 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
     out[1] = ss / (double)ws;
     out[2] = integ;
     out[3] = range;
+  }
+}
+
+__global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
+  meter_query_body(p);
+  if (p.q_done) {
+    // count this workgroup's outputs in for the device-side join: every wave's stores drained, then one
+    // agent-scope release (L2 write-back) before the add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(p.q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (p.join_ctr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    // the join: this stream's work completes only after the side stream's query workgroups (bounded)
+    for (int i = 0; i < (1 << 22); ++i) {
+      if ((int)(__hip_atomic_load(p.join_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - p.join_target) >= 0) break;
+      __builtin_amdgcn_s_sleep(4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
 }
 

@@ -80,6 +80,9 @@ struct KWeightParams {
   float* lufs_out;         // [n_cf] or nullptr
   float* weighted_out;     // [n_cf, M] or nullptr
   int mode;                // 0: K-weighting, 3: Z (no filter, no gate: professional_meters.py:228-229)
+  // when set: LUFS_inst is stored write-through and each workgroup adds 1 after it (the meter prep
+  // kernel on the side stream waits for the batch's count instead of a stream event)
+  unsigned* kw_done;
 };
 
 // Meter aggregates (meters.hip): per-channel double-buffered state (in -> out) plus per-batch scratch.
@@ -129,6 +132,16 @@ struct MeterPrepParams {
   double* gsum;     // [C, kMeterSeqCap + 1] gated-sum prefix in time order
   double* out;                     // [n_frames * C, 5]
   int parts;  // meter_query_kernel: bit 0 the LUFS meters (columns 0-3), bit 1 the true-peak meter (4)
+  // meter_prep_kernel: when set, wait until (int)(*wait_ctr - wait_target) >= 0 before reading `lufs`
+  // (the batch kernel's K-weighting workgroups count themselves in after storing their value)
+  unsigned* wait_ctr;
+  unsigned wait_target;
+  // meter_query_kernel: q_done set -> every workgroup adds 1 after its outputs are out (release);
+  // join_ctr set -> workgroup (0, 0) does not finish before (int)(*join_ctr - join_target) >= 0, so the
+  // stream it runs on completes only after the side stream's query workgroups (no stream event)
+  unsigned* q_done;
+  unsigned* join_ctr;
+  unsigned join_target;
 };
 
 struct BandParams {
@@ -174,6 +187,22 @@ struct MultiPlan {
   int n_seg;
   int res[4];
   int wg_begin[4];
+};
+
+// One launch for the per-channel-frame work of a batch of 16384-sample frames (rfkern.hip
+// batch_kernel), 512-thread workgroups. Roles: 0 K-weighting + LUFS_inst, 1 true peak, 2 the
+// 16384-point resolution (mr_res). Two segments of role groups, then the small resolutions:
+//   [seg_begin[s], seg_begin[s + 1])  groups of 8 * n_roles[s] workgroups; workgroup b of the segment
+//       runs role roles[s][(b / 8) % n_roles[s]] of channel-frame 8 (b / (8 n_roles[s])) + b % 8, so
+//       the roles of a frame land on one XCD (blockIdx % 8) and a CU sees the roles mixed
+//   [seg_begin[2], ...)  the resolutions of at most 8192 points (multi; wg_begin relative to seg_begin[2])
+// The K-weighting role counts itself into KWeightParams::kw_done when that is set.
+struct BatchPlan {
+  int seg_begin[3];
+  int n_roles[2];
+  int roles[2][3];
+  int mr_res;
+  MultiPlan multi;
 };
 
 // Fused spectrum analysis (cfg3): windowed rfft magnitude (A13) -> log-band max (A10) and raw

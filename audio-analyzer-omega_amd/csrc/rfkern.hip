@@ -20,6 +20,7 @@ namespace omega {
 OMEGA_STAMPS_DECL
 }  // namespace omega
 
+#include "kw.hpp"
 #include "regfft.hpp"
 #include "spectral.hpp"
 
@@ -31,14 +32,11 @@ template <int K>
 constexpr size_t lds_bytes() { return (RegFFT<K>::kSlots + 8) * sizeof(float2) + 64; }
 
 template <int K>
-__global__ __launch_bounds__(K / 16, 4) void truepeak_rf_kernel(SpectralParams p) {
+__device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_t cf, int t, char* smem) {
   using FFT = RegFFT<K>;
   constexpr int NTH = FFT::NTH, M = 2 * K;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* buf = reinterpret_cast<float2*>(smem);
   float* red = reinterpret_cast<float*>(smem + (FFT::kSlots + 8) * sizeof(float2));
-  const int t = threadIdx.x;
-  const int64_t cf = blockIdx.x;
   const int64_t f = cf / p.C, c = cf % p.C;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride);
   const float2* __restrict__ twK = p.tw[ilog2(K)];
@@ -123,18 +121,21 @@ __global__ __launch_bounds__(K / 16, 4) void truepeak_rf_kernel(SpectralParams p
   if (t == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
 }
 
+template <int K>
+__global__ __launch_bounds__(K / 16, 4) void truepeak_rf_kernel(SpectralParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  truepeak_rf_body<K>(p, blockIdx.x, threadIdx.x, smem);
+}
+
 // Multi-resolution frame body (A3-A5) for one resolution of K = N_r/2 complex points: windowed
 // frame straight from HBM into registers, FFT, natural-order exchange, untangle + |.| on the
 // thread's bins, weighted magnitudes out (optional, coalesced) and the combine epilogue over the
 // magnitudes parked in LDS (CombEnt plan, see spectral.hpp mrfft_frame).
 template <int K>
-__global__ __launch_bounds__(K / 16, 4) void mrfft_rf_kernel(SpectralParams p, int r) {
+__device__ __forceinline__ void mrfft_rf_body(const SpectralParams& p, int r, int64_t cf, int t, char* smem) {
   using FFT = RegFFT<K>;
   constexpr int NTH = FFT::NTH, M = 2 * K;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   float2* buf = reinterpret_cast<float2*>(smem);
-  const int t = threadIdx.x;
-  const int64_t cf = blockIdx.x;
   const int64_t f = cf / p.C, c = cf % p.C;
   const ResParam& rp = p.res[r];
   const float2* x2 = reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride + rp.offset);
@@ -203,6 +204,12 @@ __global__ __launch_bounds__(K / 16, 4) void mrfft_rf_kernel(SpectralParams p, i
   };
   if (e0 < rp.ent_end) apply(ent);
   for (int e = e0 + NTH; e < rp.ent_end; e += NTH) apply(p.ent[e]);
+}
+
+template <int K>
+__global__ __launch_bounds__(K / 16, 4) void mrfft_rf_kernel(SpectralParams p, int r) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  mrfft_rf_body<K>(p, r, blockIdx.x, threadIdx.x, smem);
 }
 
 hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s) {
@@ -391,6 +398,88 @@ hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s) {
   } else {
     return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// ---- one launch per batch of 16384-sample frames (BatchPlan, params.hpp) ----
+// The K-weighting, true-peak, 16384-point-resolution and small-resolution workgroups of a batch share
+// one grid instead of running as back-to-back full-chip kernels: every role is 512 threads with at most
+// lds_bytes<8192>() of LDS (two workgroups per CU), so a CU mixes roles -- the latency-bound
+// K-weighting scans and resolution epilogues beside the VALU-bound true-peak transforms -- and there
+// are no kernel boundaries (ramp-up / tail) between the stages. K-weighting comes first so the meter
+// aggregates on the side stream can start while the transforms run.
+constexpr int kBatchThreads = 512;
+
+// <= 8192-point resolution frames by groups of threads_for<K>() threads (mrfft_frame, spectral.hpp):
+// 2 frames of 8192 points, 4 of 4096, 8 of 2048 / 1024 / 512 per workgroup
+template <int K>
+__device__ __forceinline__ void batch_multi(const SpectralParams& p, int r, int64_t wg, int tid, float2* smem) {
+  constexpr int G = threads_for<K>();
+  constexpr int FPW = kBatchThreads / G;
+  static_assert(FPW * K * sizeof(float2) <= lds_bytes<8192>(), "LDS of one batch workgroup");
+  const int grp = tid / G;
+  const int64_t cf = wg * FPW + grp;
+  const bool valid = cf < p.n_cf;
+  mrfft_frame<K, G>(p, r, valid ? cf : p.n_cf - 1, valid, tid % G, smem + grp * K);
+}
+
+// K-weighting role (kweight_kernel's LDS, carved: pwl 2 KiB | fbuf 64 KiB | sh 32 floats | edge 20
+// floats | red 8 doubles). OMEGA_BATCH_KW_NOINLINE: a call with its own register allocation.
+#ifdef OMEGA_BATCH_KW_NOINLINE
+__device__ __attribute__((noinline))
+#else
+__device__ __forceinline__
+#endif
+void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
+  auto* pwl = reinterpret_cast<float4(*)[64]>(smem);
+  float* fbuf = reinterpret_cast<float*>(smem + 2048);
+  float* sh = reinterpret_cast<float*>(smem + 2048 + 65536);
+  float* edge = sh + 32;
+  double* red = reinterpret_cast<double*>(smem + 2048 + 65536 + 208);
+  // (one instantiation: the value is always stored write-through; a second copy of the body costs
+  // the kernel another set of spill slots)
+  kweight_body<16384, kBatchThreads, true>(kp, cf, tid, pwl, fbuf, sh, edge, red);
+  kw_count_in(kp, tid);
+}
+
+__global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams sp, KWeightParams kp, BatchPlan bp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x;
+  if (b < bp.seg_begin[2]) {
+    const int sg = b < bp.seg_begin[1] ? 0 : 1;
+    const int j = b - bp.seg_begin[sg], nr = bp.n_roles[sg];
+    const int role = bp.roles[sg][(j >> 3) % nr];
+    const int64_t cf = (int64_t)(j / (8 * nr)) * 8 + (j & 7);
+    if (cf >= sp.n_cf) return;
+    if (role == 0) {
+      batch_kw_role(kp, cf, tid, smem);
+    } else if (role == 1) {
+      truepeak_rf_body<8192>(sp, cf, tid, smem);
+    } else {
+      mrfft_rf_body<8192>(sp, bp.mr_res, cf, tid, smem);
+    }
+    return;
+  }
+  const MultiPlan& mp = bp.multi;
+  const int w = b - bp.seg_begin[2];
+  int s = 0;
+  while (s + 1 < mp.n_seg && w >= mp.wg_begin[s + 1]) ++s;
+  const int r = mp.res[s];
+  const int64_t wg = w - mp.wg_begin[s];
+  float2* buf = reinterpret_cast<float2*>(smem);
+  switch (sp.res[r].n) {
+    case 512: batch_multi<256>(sp, r, wg, tid, buf); break;
+    case 1024: batch_multi<512>(sp, r, wg, tid, buf); break;
+    case 2048: batch_multi<1024>(sp, r, wg, tid, buf); break;
+    case 4096: batch_multi<2048>(sp, r, wg, tid, buf); break;
+    case 8192: batch_multi<4096>(sp, r, wg, tid, buf); break;
+    default: break;
+  }
+}
+
+hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(batch_kernel, dim3((unsigned)grid), dim3(kBatchThreads), lds_bytes<8192>(), s, sp, kp, bp);
   return hipGetLastError();
 }
 

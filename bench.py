@@ -61,20 +61,31 @@ def cfg2_input(frames=FRAMES, w=W, seed_l=0, seed_r=1):
 
 
 def kernel_time_ms(eng, xd, reps=20):
-    """Average duration of the dominant kernel (the 8192-point true-peak kernel, one launch per batch)
-    from HIP events on the stream it is launched on (torch's current stream, bound to the context:
-    omega_true_peak on device memory launches exactly that kernel there)."""
+    """Average duration of the dominant kernel: batch_kernel, the one launch that carries all the
+    per-channel-frame work of a step (K-weighting + LUFS_inst, the four resolutions + combine, 4x true
+    peak; omega_process_frames on device memory without meters launches exactly that kernel), from
+    HIP events on the stream it is launched on (torch's current stream, bound to the context), through
+    the C ABI so the host cost per call stays below the kernel's."""
+    import ctypes
     from omega_gpu import _lib as L
     ncf = xd.numel() // W
-    out = torch.empty(ncf, dtype=torch.float32, device=xd.device)
+    keep = [torch.empty(ncf, T, device=xd.device), torch.empty(ncf, device=xd.device),
+            torch.empty(ncf, device=xd.device)]
+    outs = L.Outputs()
+    outs.combined, outs.lufs_inst, outs.true_peak_db = (t.data_ptr() for t in keep)
     lib = L.lib()
     eng._bind_stream(xd)
+
+    def call():
+        eng._check(lib.omega_process_frames(eng._ctx, xd.data_ptr(), ncf // C, C * W, W, ctypes.byref(outs),
+                                            L.MEM_DEVICE))
     for _ in range(3):
-        eng._check(lib.omega_true_peak(eng._ctx, xd.data_ptr(), ncf, W, out.data_ptr(), L.MEM_DEVICE))
+        call()
+    torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
-        eng._check(lib.omega_true_peak(eng._ctx, xd.data_ptr(), ncf, W, out.data_ptr(), L.MEM_DEVICE))
+        call()
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / reps, ncf
@@ -107,7 +118,7 @@ def cfg3_line(dev, reps=20):
     gbs = n * bpf / (ms * 1e-3) / 1e9
     return {"workload": "cfg3: 4096 mono frames x 8192, Hann rfft -> 512 log bands (A10) + chromagram (A12), fused",
             "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_batch": ms,
-            "roofline": {"bound": "hbm", "kernel": "spectra_kernel<4096>", "achieved": gbs, "peak": PEAK_HBM_GBS,
+            "roofline": {"bound": "hbm", "kernel": "spectra_rf_kernel<4096>", "achieved": gbs, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
                          "bytes_per_frame": bpf}}
 
@@ -131,11 +142,12 @@ def band_table_512(fs=FS, num_bands=512, fft_size=8192):
     return pipeline_band_table(fs, num_bands, fft_size)
 
 
-def tp_traffic():
-    """HBM bytes per true-peak launch from the newest committed counter passes (profiles/rNN_tp_traffic.json,
-    written by tools/profile_round.sh + tools/summarize_round.py), or None."""
+def kernel_traffic():
+    """HBM bytes per batch_kernel launch from the newest committed counter passes
+    (profiles/rNN_batch_traffic.json, written by tools/profile_round.sh + tools/summarize_round.py),
+    or None."""
     import glob
-    fs = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_tp_traffic.json")))
+    fs = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_batch_traffic.json")))
     if not fs:
         return None, None
     d = json.load(open(fs[-1]))
@@ -237,9 +249,9 @@ def main():
     value = total_cf / dt
 
     kt_ms, kcf = kernel_time_ms(eng, x)
-    flop_launch = FLOP_TP * kcf
+    flop_launch = (FLOP_FFT + FLOP_KW + FLOP_TP) * kcf
     achieved = flop_launch / (kt_ms * 1e-3) / 1e12
-    traffic, traffic_src = tp_traffic()
+    traffic, traffic_src = kernel_traffic()
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
@@ -254,17 +266,18 @@ def main():
                                    "combine(512) + K-weighted LUFS + 4x true peak + meter aggregates",
                        "channel_frames_per_gpu": ncf, "frame_samples": W, "target_bins": T,
                        "parallelism": f"frames sharded over {world} GPU(s)" + (", RCCL gather to rank 0" if gather else "")},
-            "roofline": {"bound": "mfma", "kernel": "truepeak_kernel<8192> (4x true peak, fp32)",
+            "roofline": {"bound": "mfma", "kernel": "batch_kernel (K-weighting + LUFS, 16k/8k/4k/1k FFT + combine, "
+                                                    "4x true peak; fp32)",
                          "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "kernel_ms": kt_ms, "flop_per_launch": flop_launch,
                          "traffic_unit": "bytes per launch (HBM, FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": kcf * (4 * W + 4),
-                         "note": "fp32 VALU/LDS-bound (fp32 MFMA peak = fp32 vector peak); algorithmic flops per "
-                                 "channel-frame from SURVEY.md §8(d) TP formula (the reference's resample "
-                                 "algorithm); kernel_ms = HIP-event average of 20 back-to-back launches on the "
-                                 "launch stream"},
+                         "algorithmic_bytes_per_launch": kcf * (4 * W + 4 * (T + 2)),
+                         "note": "fp32 VALU/LDS-bound (no MFMA: the fp32 MFMA peak equals the fp32 vector peak, "
+                                 "quoted as the roof); algorithmic flops per channel-frame = SURVEY.md §8(d) "
+                                 "FFT 1.09 M + KW 0.67 M + TP 3.33 M (the reference's resample algorithm); "
+                                 "kernel_ms = HIP-event average of 20 back-to-back launches on the launch stream"},
             "cpu_baseline": cpu,
         }
         if world == 1 and not a.no_cfg3:

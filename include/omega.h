@@ -117,9 +117,12 @@ int omega_set_stream(omega_ctx* ctx, void* hip_stream);
 /* flags: bit 0 = HIP graphs: device-memory omega_process_frames calls are captured once per distinct
  * argument set and replayed afterwards (default off: measured slower than direct launches on MI355X,
  * see DESIGN.md); bits 1-2 = stream layout:
- * 0 default: the full-chip kernels back to back on the stream, the latency-bound meter prep and LUFS
- * query kernels on a side stream; 1 everything sequentially on one stream; 2 three concurrent
- * branches (resolution kernels / true peak / K-weighting + meters). */
+ * 0 default: 16384-sample frames on direct launches run as ONE batch kernel (K-weighting, true peak
+ * and every resolution as workgroup roles of one grid) with the meter aggregates on a side stream that
+ * is ordered by device counters instead of stream events; other calls (and graph capture) as 3;
+ * 1 everything sequentially on one stream; 2 three concurrent branches (resolution kernels / true
+ * peak / K-weighting + meters); 3 the full-chip kernels back to back on the stream, the latency-bound
+ * meter prep and LUFS query kernels on a side stream joined by events. */
 int omega_set_graphs(omega_ctx* ctx, int flags);
 int omega_synchronize(omega_ctx* ctx);
 

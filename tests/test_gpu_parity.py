@@ -398,9 +398,10 @@ def test_graph_replay_matches_direct_launch():
     x = torch.from_numpy(S.cfg2_batch(8)).cuda()
     outs = []
     import os
-    for flags, fuse in ((1, "0"), (0, "0"), (2, "0"), (1, "1"), (5, "0")):
-        # graphs + default layout (meters on a side stream), direct + default, direct + sequential,
-        # graphs + fused frame kernel, graphs + three concurrent branches
+    for flags, fuse in ((1, "0"), (6, "0"), (2, "0"), (1, "1"), (5, "0"), (0, "0")):
+        # graphs (captured: full-chip kernels back to back, meters on a side stream), the same layout
+        # on direct launches, direct + sequential, graphs + fused frame kernel, graphs + three
+        # concurrent branches, direct + default (one batch_kernel launch)
         os.environ["OMEGA_FUSE"] = fuse
         try:
             eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
@@ -416,7 +417,7 @@ def test_graph_replay_matches_direct_launch():
             torch.cuda.synchronize()
             seq.append({k: v.clone() for k, v in o.items()})
         outs.append(seq)
-    for a, b in zip(outs[0], outs[1]):
+    for a, b in [*zip(outs[0], outs[1]), *zip(outs[0], outs[5])]:
         for k in a:
             assert torch.equal(a[k], b[k]), k
     for a, c in [*zip(outs[0], outs[2]), *zip(outs[0], outs[3]), *zip(outs[0], outs[4])]:
@@ -424,6 +425,43 @@ def test_graph_replay_matches_direct_launch():
         assert torch.max(torch.abs(a["true_peak_db"] - c["true_peak_db"])).item() < 1e-4
         assert torch.max(torch.abs(a["lufs_inst"] - c["lufs_inst"])).item() < 1e-3
         assert torch.max(torch.abs(a["meters"] - c["meters"])).item() < 1e-3
+
+
+def test_batch_layout_ragged_and_partial_outputs():
+    """The default layout (one batch_kernel launch: K-weighting, true-peak / 16384-point pairs, the small
+    resolutions; meter prep waiting on the K-weighting count) against the side-meter layout (separate
+    kernels, stream events): a channel-frame count that is not a multiple of the 8-frame pair groups,
+    per-resolution magnitudes and the weighted signal, subsets of the stages, and meter state carried
+    over consecutive calls -- bitwise equal."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    from omega_gpu import _lib as L
+    x = torch.from_numpy(S.cfg2_batch(13)).cuda()
+    calls = [dict(meters=True, mags=True, weighted=True), dict(meters=True), dict(true_peak=False),
+             dict(combined=False), dict(lufs=False), dict(meters=True, mags=[0])]
+    res = []
+    for flags in (0, 6):
+        eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+        eng._check(L.lib().omega_set_graphs(eng._ctx, flags))
+        seq = []
+        for kw in calls:
+            o = eng.process_frames(x, 13, 2 * 16384, 16384, **kw)
+            torch.cuda.synchronize()
+            seq.append({k: v.clone() for k, v in o.items()})
+        res.append(seq)
+    for a, b in zip(*res):
+        assert sorted(a) == sorted(b)
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    # and the first call against the oracle on a few channel-frames
+    xn = x.cpu().numpy()
+    out = {k: v.cpu().numpy() for k, v in res[0][0].items()}
+    for f, c in ((0, 0), (6, 1), (12, 1)):
+        _, comb, li, tp = R.full_frame(xn[f, c])
+        cf = 2 * f + c
+        assert normwise(out["combined"][cf], comb) < SPEC_TOL
+        assert abs(out["lufs_inst"][cf] - li) < LU_TOL
+        assert abs(out["true_peak_db"][cf] - tp) < TP_TOL_DB
 
 
 def test_spectra_cfg3_vs_oracle():

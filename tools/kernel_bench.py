@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one stage of the cfg2 hot path in isolation (for rocprofv3 counter passes and A/B timing).
 
-  python tools/kernel_bench.py {tp,kw,mrfft,meters,all,host,spectra} [--reps N]
+  python tools/kernel_bench.py {batch,tp,kw,mrfft,meters,all,host,spectra} [--reps N]
 """
 import argparse
 import os
@@ -45,7 +45,14 @@ def main():
         so = {"bands": torch.empty(4096, 512, device="cuda"),
               "chroma": torch.empty(4096, 12, dtype=torch.float64, device="cuda")}
 
+    outs = L.Outputs()
+    outs.combined, outs.lufs_inst, outs.true_peak_db = comb.data_ptr(), out["li"].data_ptr(), out["tp"].data_ptr()
+
     def run():
+        if a.stage == "batch":  # one batch_kernel launch: the step's per-channel-frame work, no meters
+            import ctypes
+            eng._check(lib.omega_process_frames(eng._ctx, x.data_ptr(), 256, 2 * 16384, 16384, ctypes.byref(outs),
+                                                L.MEM_DEVICE))
         if a.stage == "spectra":
             e3.spectra(x3, "hann", bands=bt, chroma=True, out=so)
         if a.stage == "host":  # host buffers in and out: PCIe-inclusive rate of the full path

@@ -6,7 +6,7 @@
   rNN_bench_dispatches.md     per-kernel dispatch averages; the true-peak dispatches split into the
                               in-pipeline ones (overlapped with the other streams) and the roofline
                               probe's back-to-back ones (what bench.py's roofline.kernel_ms times)
-  rNN_tp_traffic.json         HBM bytes per true-peak launch from FETCH_SIZE / WRITE_SIZE passes
+  rNN_batch_traffic.json      HBM bytes per batch_kernel launch from FETCH_SIZE / WRITE_SIZE passes
 
   python tools/summarize_round.py 01
 """
@@ -19,7 +19,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "gpurun_out", "round")
-TP = "truepeak_kernel<8192, 1024>"
+TP = "batch_kernel"
 
 
 def short(n):
@@ -43,15 +43,15 @@ def main(rnd):
     for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
         lines.append(f"| `{k}` | {len(v)} | {sum(v) / len(v):.1f} | {min(v):.1f} | {max(v):.1f} |")
     tp = per.get(TP, [])
-    # bench.py: 55 pipeline steps (5 warmup + 50 timed) each launch one true-peak kernel inside the
-    # replayed graph, then the roofline probe launches it 3 + 20 times back to back, alone
+    # bench.py: 55 pipeline steps (5 warmup + 50 timed) each launch one batch kernel, then the
+    # roofline probe launches it 3 + 20 times back to back, without the meter kernels beside it
     steps = 55
     pipe, probe = tp[:steps], tp[steps:]
     if probe:
         timed = probe[3:]
-        lines += ["", f"True-peak kernel `{TP}`:", "",
-                  f"- in the pipeline (overlapped with the resolution, K-weighting and meter kernels on other "
-                  f"streams): {len(pipe)} dispatches, avg {sum(pipe) / len(pipe):.1f} us",
+        lines += ["", f"Batch kernel `{TP}` (all per-channel-frame work of a step in one launch):", "",
+                  f"- in the pipeline (the meter kernels run beside it on a side stream): {len(pipe)} dispatches, "
+                  f"avg {sum(pipe) / len(pipe):.1f} us",
                   f"- roofline probe (alone, back to back; bench.py `roofline.kernel_ms` times these 20 with HIP "
                   f"events): {len(timed)} dispatches, avg {sum(timed) / len(timed):.1f} us"]
     b = json.loads([ln for ln in open(os.path.join(SRC, "stats.json")) if ln.startswith("{")][-1]) \
@@ -65,14 +65,14 @@ def main(rnd):
         v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if short(r["Kernel_Name"]) == TP]
         tr[c] = sum(v) / len(v)
         tr[c + "_dispatches"] = len(v)
-    out = {"kernel": TP, "command": "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace -- python tools/kernel_bench.py tp --reps 20",
+    out = {"kernel": TP, "command": "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace -- python tools/kernel_bench.py batch --reps 20",
            "fetch_size_kib": tr["FETCH_SIZE"], "write_size_kib": tr["WRITE_SIZE"],
            "traffic_bytes": 2 * tr["FETCH_SIZE"] * 1024 + tr["WRITE_SIZE"] * 1024,
            "dispatches": tr["FETCH_SIZE_dispatches"],
            "method": "separate --pmc passes; FETCH_SIZE (KiB) doubled for gfx950 (MI355X_MICROARCH.md: it reports "
                      "half the bytes of wide streaming reads), WRITE_SIZE (KiB) as reported",
-           "algorithmic_bytes": 512 * 16384 * 4 + 512 * 4}
-    json.dump(out, open(os.path.join(dst, f"r{rnd}_tp_traffic.json"), "w"), indent=1)
+           "algorithmic_bytes": 512 * (16384 * 4 + 4 * (512 + 2))}
+    json.dump(out, open(os.path.join(dst, f"r{rnd}_batch_traffic.json"), "w"), indent=1)
     print(open(os.path.join(dst, f"r{rnd}_bench_dispatches.md")).read())
     print(json.dumps(out, indent=1))
 
