@@ -735,10 +735,10 @@ bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams&
 // count, kw_done) and the LUFS meters (their workgroups count themselves in). The true-peak meter's
 // first workgroup waits for that count, so `s` completes only after fork[0]'s work: no stream events
 // anywhere (each event record / wait cost ~7-13 us of idle GPU between kernels). cfg2 step on MI355X:
-// 96.5 us (order 3); 98.0 (2: K-weighting mixed with the true peaks), 112.9 (1: all three mixed), 106.3
-// (0: K-weighting as its own kernel first; it does not spill there but mixes with nothing); the
-// side-meter layout with events 99.7. Mixing the latency-bound K-weighting scans with transform work
-// is what pays; the K-weighting body spills in the batch kernel (128 VGPRs at two workgroups per CU).
+// 79.5 us (order 3); 85.2 (2: K-weighting mixed with the true peaks), 110.4 (0: K-weighting as its own
+// kernel first: it mixes with nothing); the side-meter layout with events 99.2. Mixing the
+// latency-bound K-weighting scans with transform work is what pays (K-weighting alone 25.7 us, the
+// true peak 37, the resolutions 26.5; one batch launch of all three 73.9).
 int enqueue_batch(omega_ctx* c, const SpectralParams& sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
                   const float* tp, double* meters, hipStream_t s, int mr, bool do_tp, bool do_kw) {
   const int64_t n = sp.n_cf;

@@ -75,7 +75,7 @@ __device__ __forceinline__ void mv4(const float4 m, float a0, float a1, float& r
 // entering the first processed sample. On return u holds the outputs and (fin0, fin1) the state
 // after the last processed sample (all threads). pwl[l] = P^(l+1) (LDS). sh: >= 4*NW floats of LDS;
 // the forward and the backward pass use separate halves, so the pass needs a single barrier.
-template <int L, int NTH, bool REV, int SB>
+template <int L, int NTH, bool REV, int SB, bool OPQ = false>
 __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, const float4* pwl, float sin0,
                                              float sin1, float* sh, int tid, float& fin0, float& fin1) {
   constexpr int NW = NTH / 64;
@@ -175,7 +175,14 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
   const float i1 = vl == 0 ? k1 : p1;
   OMEGA_STAMP(SB + 3);
   // 5) the chunk from its true incoming state: each sub-chunk's incoming state follows from the
-  // previous one's (A^LS in + its zero-state end state), then all run interleaved
+  // previous one's (A^LS in + its zero-state end state), then all run interleaved. (The samples pass
+  // through an opaque copy first (OPQ, the batch kernel): otherwise the compiler keeps step 1's B1 * u
+  // products live across the scan for reuse here -- L more live registers, spilled there; the
+  // standalone kernel runs faster without the copy.)
+  if constexpr (OPQ) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) asm volatile("" : "+v"(u[i]));
+  }
   {
     float r0[S], r1[S];
     r0[0] = i0;
@@ -197,7 +204,7 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
 }
 
 // filtfilt of the block-distributed signal u (in place). e[0..9] = u[0..9], e[10..19] = u[M-10..M-1].
-template <int L, int NTH, int SB>
+template <int L, int NTH, int SB, bool OPQ = false>
 __device__ __forceinline__ void filtfilt(float (&u)[L], const BiquadTab* __restrict__ tg, const float4* pwl, const float* e,
                                          float* sh, int tid) {
   constexpr int E = 9;
@@ -208,7 +215,7 @@ __device__ __forceinline__ void filtfilt(float (&u)[L], const BiquadTab* __restr
 #pragma unroll
   for (int i = 0; i < E; ++i) bq_step(t, 2.f * u0 - e[E - i], s0, s1);
   float f0, f1;
-  lfilter_pass<L, NTH, false, SB>(u, t, pwl, s0, s1, sh, tid, f0, f1);
+  lfilter_pass<L, NTH, false, SB, OPQ>(u, t, pwl, s0, s1, sh, tid, f0, f1);
   // right odd extension ext[M+9+i] = 2u[M-1] - u[M-2-i]: forward outputs, then the backward start
   float yr[E];
 #pragma unroll
@@ -217,17 +224,25 @@ __device__ __forceinline__ void filtfilt(float (&u)[L], const BiquadTab* __restr
   s1 = t.zi1 * yr[E - 1];
 #pragma unroll
   for (int i = E - 1; i >= 0; --i) bq_step(t, yr[i], s0, s1);
-  lfilter_pass<L, NTH, true, SB + 5>(u, t, pwl, s0, s1, sh, tid, f0, f1);
+  lfilter_pass<L, NTH, true, SB + 5, OPQ>(u, t, pwl, s0, s1, sh, tid, f0, f1);
 }
 
-template <int L, int NTH>
+template <int L, int NTH, bool OPQ = false>
 __device__ __forceinline__ void gather_edges(const float (&u)[L], float* e, int tid) {
   constexpr int M = L * NTH;
-  static_for<0, L>([&](auto i) {
-    const int n = tid * L + i;
-    if (n < 10) e[n] = u[i];
-    if (n >= M - 10) e[10 + n - (M - 10)] = u[i];
-  });
+  if constexpr (OPQ && L >= 10) {
+    // the first and the last thread hold the edges: 20 stores behind two branches (a per-element
+    // predicate costs address registers for every one of the L elements, spilled in the batch
+    // kernel; the standalone kernel measured faster with the per-element form)
+    if (tid == 0) static_for<0, 10>([&](auto i) { e[i] = u[i]; });
+    if (tid == NTH - 1) static_for<0, 10>([&](auto i) { e[10 + i] = u[L - 10 + i]; });
+  } else {
+    static_for<0, L>([&](auto i) {
+      const int n = tid * L + i;
+      if (n < 10) e[n] = u[i];
+      if (n >= M - 10) e[10 + n - (M - 10)] = u[i];
+    });
+  }
 }
 
 // LUFS_inst store of thread 0. PUB: write-through (sc1) agent-scope store, so that a counter add
@@ -252,7 +267,7 @@ __device__ __forceinline__ void kw_count_in(const KWeightParams& p, int tid) {
 // K-weighting of channel-frame cf by a workgroup of NTH threads (all of them), chunk L = M / NTH
 // (the host tables must be built for that L). LDS from the caller: pwl[2][64] scan powers, fbuf[M]
 // parking for f (element-major), sh[4 * NW], edge[20], red[NW].
-template <int M, int NTH, bool PUB = false>
+template <int M, int NTH, bool PUB = false, bool OPQ = false>
 __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf, int tid, float4 (*pwl)[64], float* fbuf,
                                              float* sh, float* edge, double* red) {
   constexpr int L = M / NTH;
@@ -298,17 +313,17 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
     if (tid == 0 && p.lufs_out) put_lufs<PUB>(p.lufs_out, cf, -100.0f);
     return;
   }
-  gather_edges<L, NTH>(u, edge, tid);
+  gather_edges<L, NTH, OPQ>(u, edge, tid);
   __syncthreads();
   OMEGA_STAMP(3);
-  filtfilt<L, NTH, 4>(u, p.hp, pwl[0], edge, sh, tid);
+  filtfilt<L, NTH, 4, OPQ>(u, p.hp, pwl[0], edge, sh, tid);
   // u = f (high-passed): park it in LDS, run the shelf stage on u
   static_for<0, L>([&](auto i) { fbuf[i * NTH + tid] = u[i]; });
   __syncthreads();
-  gather_edges<L, NTH>(u, edge, tid);
+  gather_edges<L, NTH, OPQ>(u, edge, tid);
   __syncthreads();
   OMEGA_STAMP(14);
-  filtfilt<L, NTH, 15>(u, p.shelf, pwl[1], edge, sh, tid);
+  filtfilt<L, NTH, 15, OPQ>(u, p.shelf, pwl[1], edge, sh, tid);
   OMEGA_STAMP(25);
   float acc = 0.f;
   static_for<0, L>([&](auto i) {

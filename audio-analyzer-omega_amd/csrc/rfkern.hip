@@ -438,7 +438,7 @@ void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
   double* red = reinterpret_cast<double*>(smem + 2048 + 65536 + 208);
   // (one instantiation: the value is always stored write-through; a second copy of the body costs
   // the kernel another set of spill slots)
-  kweight_body<16384, kBatchThreads, true>(kp, cf, tid, pwl, fbuf, sh, edge, red);
+  kweight_body<16384, kBatchThreads, true, true>(kp, cf, tid, pwl, fbuf, sh, edge, red);
   kw_count_in(kp, tid);
 }
 

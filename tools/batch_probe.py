@@ -41,7 +41,7 @@ def main():
     ncf = 512
     o = {"combined": torch.empty(ncf, 512, device="cuda"), "lufs_inst": torch.empty(ncf, device="cuda"),
          "true_peak_db": torch.empty(ncf, device="cuda")}
-    order = os.environ.get("OMEGA_BATCH_ORDER", "0")
+    order = os.environ.get("OMEGA_BATCH_ORDER", "default")
     for mode, name in ((0, f"batch/{order}"), (6, "separate")):
         eng = Engine(NORTHSTAR_RESOLUTIONS, 48000, 20000, target_bins=512, n_channels=2)
         eng._check(L.lib().omega_set_graphs(eng._ctx, mode))
