@@ -40,6 +40,7 @@ hipError_t launch_bands(const BandParams& p, hipStream_t s);
 hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int hi, const double* mat, double* out,
                          hipStream_t s);
 hipError_t launch_combine(const CombineParams& p, hipStream_t s);
+hipError_t launch_drum(const DrumParams& p, hipStream_t s);
 hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s);
 }  // namespace omega
 
@@ -222,6 +223,14 @@ struct omega_ctx {
     int* goff = nullptr;
   } ctab;
   int n_cu = 0;
+  // drum-feature stream state (omega_drum_features), double-buffered, for drum_bins bins per frame
+  int drum_bins = 0, drum_cur = 0;
+  float* d_dprev[2] = {};
+  float* d_dhist[2] = {};
+  int* d_dlen[2] = {};
+  long long* d_dpos[2] = {};
+  float* d_dflux = nullptr;
+  int64_t dflux_cap = 0;
   // meter state (double-buffered)
   float* d_hist_l[2] = {};
   float* d_hist_t[2] = {};
@@ -976,6 +985,91 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   if (!e) e = build_meter_state(c);
   *out = c;
   return e;
+}
+
+int omega_drum_reset(omega_ctx* c) {
+  if (!c) return OMEGA_EINVAL;
+  if (!c->drum_bins) return 0;
+  HIPC(c, hipSetDevice(c->device));
+  for (int b = 0; b < 2; ++b) {
+    HIPC(c, hipMemsetAsync(c->d_dlen[b], 0, kDrumBands * sizeof(int), c->stream));
+    HIPC(c, hipMemsetAsync(c->d_dpos[b], 0, sizeof(long long), c->stream));
+  }
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int omega_drum_features(omega_ctx* c, const float* mag, int64_t n_frames, int32_t n_bins, int64_t mag_stride,
+                        double sensitivity, double* out, int mem) {
+  if (!c || !out) return OMEGA_EINVAL;
+  if (!mag || n_frames < 0 || n_bins < 2 || mag_stride < n_bins)
+    return fail(c, OMEGA_EINVAL, "drum features: bad magnitude layout (n_bins %d, stride %lld)", n_bins,
+                (long long)mag_stride);
+  if (c->drum_bins && c->drum_bins != n_bins)
+    return fail(c, OMEGA_EINVAL, "drum features: the stream has %d bins per frame, got %d (omega_drum_reset "
+                "does not change it; create another context)", c->drum_bins, n_bins);
+  if (n_frames == 0) return 0;
+  HIPC(c, hipSetDevice(c->device));
+  if (!c->drum_bins) {
+    for (int b = 0; b < 2; ++b) {
+      int e = dalloc(c, &c->d_dprev[b], (size_t)n_bins);
+      if (!e) e = dalloc(c, &c->d_dhist[b], (size_t)kDrumBands * kDrumHist);
+      if (!e) e = dalloc(c, &c->d_dlen[b], kDrumBands);
+      if (!e) e = dalloc(c, &c->d_dpos[b], 1);
+      if (e) return e;
+    }
+    c->drum_bins = n_bins;
+    const int e = omega_drum_reset(c);
+    if (e) return e;
+  }
+  if (n_frames > c->dflux_cap) {
+    const int e = dalloc(c, &c->d_dflux, (size_t)n_frames * kDrumBands);
+    if (e) return e;
+    c->dflux_cap = n_frames;
+  }
+  std::vector<HostOut> outs;
+  const float* dm = mag;
+  double* dout = out;
+  if (mem == OMEGA_MEM_HOST) {
+    int e = stage_in(c, 0, mag, (size_t)((n_frames - 1) * mag_stride + n_bins) * sizeof(float),
+                     reinterpret_cast<const void**>(&dm));
+    if (!e) e = stage_out(c, 1, out, (size_t)n_frames * kDrumCols, outs, &dout);
+    if (e) return e;
+  }
+  // drum_detection.py: bins int(f * len / nyquist) (:86-96, :240-259, :218-219), numpy slices clamp
+  const double fs = c->cfg.sample_rate, ny = fs / 2;
+  const double bands[kDrumBands][2] = {{20, 60}, {60, 120}, {2000, 5000}, {150, 400}, {400, 1000}, {2000, 8000},
+                                       {8000, 15000}};
+  const double mult[kDrumBands] = {2.8, 2.8, 2.8, 2.5, 2.3, 2.0, 0.0};  // :78, :295, :300, :305
+  DrumParams p{};
+  p.mag = dm;
+  p.n = n_frames;
+  p.stride = mag_stride;
+  p.n_bins = n_bins;
+  auto bin = [&](double f) { return std::min(n_bins, (int)(f * n_bins / ny)); };
+  for (int b = 0; b < kDrumBands; ++b) {
+    p.bs[b] = bin(bands[b][0]);
+    p.be[b] = std::max(p.bs[b], bin(bands[b][1]));
+    p.mult[b] = (float)(sensitivity * mult[b]);
+  }
+  p.cs = bin(150.0);
+  p.ce = std::max(p.cs, bin(15000.0));
+  p.fstep = 1.0 / ((2.0 * n_bins - 1.0) * (1.0 / fs));  // np.fft.rfftfreq(2 n - 1, 1 / fs) spacing
+  const int a = c->drum_cur, b = a ^ 1;
+  p.prev_in = c->d_dprev[a];
+  p.prev_out = c->d_dprev[b];
+  p.hist_in = c->d_dhist[a];
+  p.hist_out = c->d_dhist[b];
+  p.len_in = c->d_dlen[a];
+  p.len_out = c->d_dlen[b];
+  p.pos_in = c->d_dpos[a];
+  p.pos_out = c->d_dpos[b];
+  p.flux = c->d_dflux;
+  p.out = dout;
+  HIPC(c, launch_drum(p, c->stream));
+  c->drum_cur = b;
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
 }
 
 void omega_destroy(omega_ctx* c) {

@@ -229,6 +229,33 @@ struct SpectraParams {
   const float2* tw[kMaxLog2];
 };
 
+// Drum-detection spectral features (drum.hip): 7 flux bands (kick sub / body /
+// click, snare fundamental / body / snap / rattle), the snare centroid range, and one stream's state
+// (previous magnitude frame, 21-deep flux histories, frames seen), double-buffered (in -> out).
+constexpr int kDrumBands = 7;
+constexpr int kDrumHist = 21;
+constexpr int kDrumCols = 14;
+
+struct DrumParams {
+  const float* mag;
+  int64_t n, stride;
+  int n_bins;
+  int bs[kDrumBands], be[kDrumBands];  // band bins [bs, be)
+  int cs, ce;                          // centroid bins
+  double fstep;                        // rfftfreq(2 n_bins - 1) spacing: fs / (2 n_bins - 1)
+  float mult[kDrumBands];              // float32(sensitivity * multiplier); 0: no threshold
+  const float* prev_in;
+  float* prev_out;                     // [n_bins]
+  const float* hist_in;
+  float* hist_out;                     // [kDrumBands][kDrumHist], oldest first
+  const int* len_in;
+  int* len_out;                        // [kDrumBands]
+  const long long* pos_in;
+  long long* pos_out;                  // frames of the stream seen before / after this call
+  float* flux;                         // [n, kDrumBands] scratch
+  double* out;                         // [n, kDrumCols] (oracle DRUM_COLUMNS order)
+};
+
 struct RfftParams {
   const float* x;
   int64_t n;

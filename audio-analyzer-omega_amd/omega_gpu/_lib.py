@@ -79,6 +79,9 @@ EXPORTS = {
     "omega_bands_apply": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
                                     C.c_int]),
     "omega_chroma": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_double, C.c_void_p, C.c_int]),
+    "omega_drum_features": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int64, C.c_double,
+                                      C.c_void_p, C.c_int]),
+    "omega_drum_reset": (C.c_int, [C.c_void_p]),
     "omega_rfft": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                              C.c_int]),
 }

@@ -241,6 +241,24 @@ class Engine:
                                           L.MEM_DEVICE if dev else L.MEM_HOST))
         return o
 
+    def drum_features(self, mags, sensitivity: float = 1.0, out=None):
+        """Kick + snare spectral features of consecutive magnitude frames of one stream (omega_drum_features):
+        [F, 14] float64 in DRUM_COLUMNS order; the stream state carries over to the next call
+        (reset_drums starts a new stream). mags: [F, n_bins] float32, host numpy or device torch."""
+        dev = _is_torch(mags)
+        if not dev:
+            mags = np.ascontiguousarray(mags, dtype=np.float32)
+        F, n = mags.shape
+        o = out if out is not None else self._alloc(mags, (F, 14), np.float64)
+        if dev:
+            self._bind_stream(mags)
+        self._check(L.lib().omega_drum_features(self._ctx, _ptr(mags), int(F), int(n), int(mags.stride(0) if dev else n),
+                                                float(sensitivity), _ptr(o), L.MEM_DEVICE if dev else L.MEM_HOST))
+        return o
+
+    def reset_drums(self):
+        self._check(L.lib().omega_drum_reset(self._ctx))
+
     def chroma_raw(self, spec: np.ndarray, df: float) -> np.ndarray:
         s = np.ascontiguousarray(np.atleast_2d(spec), dtype=np.float32)
         out = np.empty((s.shape[0], 12), np.float64)

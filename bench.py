@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
+                    help="processes of the all-cores CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 (HBM-roofline) line")
     return ap.parse_args()
 
@@ -123,6 +125,35 @@ def cfg3_line(dev, reps=20):
                          "bytes_per_frame": bpf}}
 
 
+def drums_line(dev, reps=20, n=4096, bins=1025):
+    """SURVEY.md §8(f) row 1 (drum-detection features): one call over n consecutive magnitude frames
+    of one stream (kick/snare band flux, adaptive thresholds, centroid), device-resident. Bytes per
+    frame: the magnitude row in + 14 float64 out."""
+    from omega_gpu import Engine
+    rng = np.random.default_rng(5)
+    mags = torch.from_numpy(np.abs(rng.standard_normal((n, bins))).astype(np.float32)).to(dev)
+    eng = Engine(sample_rate=FS, device=dev.index or 0)
+    out = torch.empty(n, 14, dtype=torch.float64, device=dev)
+    for _ in range(3):
+        eng.drum_features(mags, out=out)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        eng.drum_features(mags, out=out)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    bpf = 4 * bins + 8 * 14
+    gbs = n * bpf / (ms * 1e-3) / 1e9
+    return {"workload": f"drum features: {n} consecutive frames x {bins} bins of one stream (kick 3 + snare 4 band "
+                        "flux, adaptive thresholds, spectral centroid)",
+            "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_call": ms,
+            "roofline": {"bound": "hbm", "kernel": "drum_flux_kernel + drum_thr_kernel", "achieved": gbs,
+                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
+                         "bytes_per_frame": bpf}}
+
+
 def cfg3_input(n, m):
     """BASELINE cfg3 synthetic frames (same generator as oracle/signals.cfg3_batch): even frames a
     0.5-amplitude C-major triad, odd frames 0.1 N(0,1) (seed 1234)."""
@@ -177,11 +208,47 @@ def cpu_baseline(seconds):
                       f"4x TP + meter deques), {dt:.1f} s, OMP_NUM_THREADS=1"}
 
 
+def _cpu_worker(args):
+    """One CPU-baseline process: its own channel of the cfg2 frames (oracle loop with meter state)."""
+    seconds, c, seed = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from oracle import omega_ref as R
+    x = cfg2_input(16, seed_l=seed, seed_r=seed + 1)
+    st = R.MeterState(FS)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        fr = x[n % 16, c]
+        _, _, li, tp = R.full_frame(fr)
+        st.update(fr, li, tp)
+        n += 1
+        if time.perf_counter() - t0 > seconds and n >= 4:
+            break
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline_all_cores(seconds, procs):
+    """SURVEY.md §8(d)'s second CPU mode: the same oracle loop in `procs` processes (one stream each),
+    forked before this process touches the GPU; aggregate channel-frames/s."""
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(seconds, i % 2, 2 * (i // 2)) for i in range(procs)])
+    n = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return {"value": n / wall, "unit": "channel-frames/s", "cores": procs, "kind": "port",
+            "sample": f"{n} channel-frames of cfg2 over {procs} processes (one stream each, oracle loop with "
+                      f"meter state), {wall:.1f} s, OMP_NUM_THREADS=1"}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu_all = None
+    if world == 1 and not a.no_cpu_baseline and a.cpu_procs > 1:
+        # before any GPU call: the workers are forked from this process
+        cpu_all = cpu_baseline_all_cores(a.cpu_seconds, a.cpu_procs)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -279,9 +346,11 @@ def main():
                                  "FFT 1.09 M + KW 0.67 M + TP 3.33 M (the reference's resample algorithm); "
                                  "kernel_ms = HIP-event average of 20 back-to-back launches on the launch stream"},
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
         }
         if world == 1 and not a.no_cfg3:
             line["cfg3"] = cfg3_line(dev)
+            line["drums"] = drums_line(dev)
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -24,6 +24,8 @@
  *   omega_chroma           ChromagramAnalyzer.compute_chromagram      omega4/panels/chromagram.py:109-159
  *   omega_rfft             BatchedFFTProcessor process_batch (CPU/CuPy branches) omega4/optimization/batched_fft_processor.py:148-285
  *   omega_spectra          omega_rfft -> omega_bands_apply (MAX) + omega_chroma fused in one pass (cfg3)
+ *   omega_drum_features    EnhancedKickDetector / EnhancedSnareDetector band flux, adaptive thresholds and
+ *                          spectral centroid  omega4/analyzers/drum_detection.py:47-103, :212-305 (§8(f) row 1)
  *
  * Conventions:
  *   - every function returns 0 on success and a negative omega_status on error; the message is
@@ -188,6 +190,19 @@ int omega_rfft(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t win
  * each frame once. Any output may be NULL: bands_out [n, n_out], chroma_out [n, 12], mag_out
  * [n, m/2+1]. Replaces the BatchedFFTProcessor -> map_to_bands / compute_chromagram chain
  * (batched_fft_processor.py:148-285, pipeline.py:295-335, chromagram.py:109-159). ---- */
+/* Drum-detection spectral features of consecutive magnitude frames of ONE stream (SURVEY.md §8(f)
+ * row 1) -- replaces the per-frame feature part of omega4/analyzers/drum_detection.py
+ * EnhancedKickDetector.detect_kick_onset :80-103 (calculate_band_flux :47-67,
+ * calculate_adaptive_threshold :69-78) and EnhancedSnareDetector.detect_snare_onset :268-305
+ * (calculate_multi_band_flux :231-266, calculate_spectral_centroid :212-229); the onset decisions read
+ * the wall clock and stay with the caller. mag: n_frames rows of n_bins float32 magnitudes, row
+ * stride mag_stride floats. out: [n_frames, 14] float64 = kick sub/body/click flux, kick sub/body/click
+ * threshold, snare fundamental/body/snap/rattle flux, snare fundamental/body/snap threshold, snare
+ * spectral centroid (Hz). The context keeps the stream state (previous frame, 21-deep flux histories)
+ * across calls; omega_drum_reset starts a new stream. n_bins is fixed per context. */
+int omega_drum_features(omega_ctx* ctx, const float* mag, int64_t n_frames, int32_t n_bins, int64_t mag_stride,
+                        double sensitivity, double* out, int mem);
+int omega_drum_reset(omega_ctx* ctx);
 int omega_spectra(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t window, omega_bands* bands,
                   float* bands_out, double* chroma_out, float* mag_out, int mem);
 

@@ -45,6 +45,7 @@ def _import_reference():
     from omega4.optimization.freq_mapper import PrecomputedFrequencyMapper
     from omega4.panels.chromagram import ChromagramAnalyzer
     from omega4.optimization.batched_fft_processor import BatchedFFTProcessor
+    from omega4.analyzers.drum_detection import EnhancedKickDetector, EnhancedSnareDetector
     return SimpleNamespace(**locals())
 
 
@@ -208,11 +209,51 @@ def gen_batched(R):
     np.savez_compressed(os.path.join(OUT, "batched.npz"), **d)
 
 
+def drum_signal(n_frames, n_fft=2048, hop=512, seed=7):
+    """Hann-windowed magnitude frames of a synthetic drum track: a decaying 55 Hz kick every 8 frames,
+    a noise snare (with a 200 Hz body) every 8 frames offset by 4, a quiet noise floor."""
+    rng = np.random.default_rng(seed)
+    n = n_fft + hop * (n_frames - 1)
+    t = np.arange(n) / FS
+    x = 0.01 * rng.standard_normal(n)
+    for k in range(0, n_frames, 8):
+        t0 = k * hop
+        d = np.exp(-np.arange(n - t0) / (0.05 * FS))
+        x[t0:] += 0.8 * np.sin(2 * np.pi * 55 * t[: n - t0]) * d
+        s0 = t0 + 4 * hop
+        if s0 < n:
+            d2 = np.exp(-np.arange(n - s0) / (0.02 * FS))
+            x[s0:] += (0.3 * rng.standard_normal(n - s0) + 0.3 * np.sin(2 * np.pi * 200 * t[: n - s0])) * d2
+    w = np.hanning(n_fft)
+    return np.stack([np.abs(np.fft.rfft(x[i * hop:i * hop + n_fft] * w)) for i in range(n_frames)]).astype(np.float32)
+
+
+def gen_drums(R):
+    """EnhancedKickDetector / EnhancedSnareDetector run frame by frame on the same magnitudes: the
+    fluxes, kick thresholds (the click threshold through the detector's own calculate_adaptive_threshold)
+    and the snare spectral centroid. The onset flags read the wall clock and are not recorded."""
+    d = {"versions": VERSIONS}
+    for name, nf, nfft in (("drums_1025", 40, 2048), ("drums_2049", 24, 4096)):
+        mags = drum_signal(nf, nfft)
+        kd, sd = R.EnhancedKickDetector(FS), R.EnhancedSnareDetector(FS)
+        rows = []
+        for m in mags:
+            k = kd.detect_kick_onset(m)
+            s = sd.detect_snare_onset(m)
+            rows.append([k["sub_flux"], k["body_flux"], k["click_flux"], k["sub_threshold"], k["body_threshold"],
+                         kd.calculate_adaptive_threshold(kd.click_flux_history),
+                         s["fundamental_flux"], s["body_flux"], s["snap_flux"], s["rattle_flux"],
+                         s["spectral_centroid"]])
+        d[f"{name}/mags"] = mags
+        d[f"{name}/out"] = np.array(rows, dtype=np.float64)
+    np.savez_compressed(os.path.join(OUT, "drums.npz"), **d)
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in (gen_mrfft, gen_meters, gen_bands, gen_chroma, gen_batched):
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums"))]:
         g(R)
         print("wrote", g.__name__)

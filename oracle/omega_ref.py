@@ -572,3 +572,92 @@ def full_frame(x: np.ndarray, configs=NORTHSTAR_CONFIGS, fs=48000, target_bins=5
     res = mrfft_frame(x, configs, fs)
     comb, _ = combine(res, configs, fs, 20000, target_bins)
     return res, comb, lufs_instant(x, fs), true_peak(x)
+
+
+# ----------------------------------------------------------------------------------------------
+# drum-detection spectral features -- band flux, adaptive thresholds and the
+# snare spectral centroid (omega4/analyzers/drum_detection.py: EnhancedKickDetector :19-28, :47-103;
+# EnhancedSnareDetector :183-194, :212-266, :279-305). The onset decisions themselves read the wall
+# clock (time.time(), :82, :270) and are not part of the data-parallel path.
+# ----------------------------------------------------------------------------------------------
+
+KICK_BANDS = ((20, 60), (60, 120), (2000, 5000))                       # drum_detection.py:20-22
+SNARE_BANDS = ((150, 400), (400, 1000), (2000, 8000), (8000, 15000))   # :183-186
+SNARE_MULT = (2.5, 2.3, 2.0)                                           # :295, :300, :305
+DRUM_COLUMNS = ("kick_sub_flux", "kick_body_flux", "kick_click_flux",
+                "kick_sub_threshold", "kick_body_threshold", "kick_click_threshold",
+                "snare_fundamental_flux", "snare_body_flux", "snare_snap_flux", "snare_rattle_flux",
+                "snare_fundamental_threshold", "snare_body_threshold", "snare_snap_threshold",
+                "snare_centroid")
+
+
+def drum_band_bins(band, n_bins: int, fs: float = 48000):
+    """int(f * len(magnitude) / nyquist) for both edges (:86-96, :240-259)."""
+    ny = fs / 2
+    return int(band[0] * n_bins / ny), int(band[1] * n_bins / ny)
+
+
+def adaptive_threshold(hist, mult: float, sensitivity: float = 1.0):
+    """median + sensitivity * mult * MAD over the history, 0 below 10 values (:69-78, :290-305)."""
+    if len(hist) < 10:
+        return 0.0
+    a = np.array(list(hist))
+    med = np.median(a)
+    mad = np.median(np.abs(a - med))
+    return med + sensitivity * mult * mad
+
+
+class DrumFluxState:
+    """One stream's kick + snare feature state: previous magnitude frame and the 21-deep flux
+    histories, updated per frame exactly as detect_kick_onset / detect_snare_onset do."""
+
+    def __init__(self, fs: float = 48000, sensitivity: float = 1.0):
+        self.fs, self.sens = fs, sensitivity
+        self.prev_k = None  # EnhancedKickDetector.prev_magnitude
+        self.prev_s = None  # EnhancedSnareDetector.prev_magnitude
+        self.hk = [deque(maxlen=21) for _ in KICK_BANDS]
+        self.hs = [deque(maxlen=21) for _ in SNARE_BANDS]
+
+    def update(self, mag: np.ndarray) -> np.ndarray:
+        n = len(mag)
+        # kick (:85-103): on the first frame the sub band sets prev and returns 0 WITHOUT appending
+        # (:51-53); body and click then see prev == mag and append 0
+        kf = []
+        for b, band in enumerate(KICK_BANDS):
+            s, e = drum_band_bins(band, n, self.fs)
+            if self.prev_k is None:
+                self.prev_k = mag.copy()
+                kf.append(0.0)
+                continue
+            f = np.sum(np.maximum(mag[s:e] - self.prev_k[s:e], 0))
+            self.hk[b].append(f)
+            kf.append(f)
+        self.prev_k = mag.copy()
+        kt = [adaptive_threshold(h, 2.8, self.sens) for h in self.hk]
+        # snare (:231-266): zeros on the first frame (prev set), appended by detect_snare_onset
+        if self.prev_s is None:
+            self.prev_s = mag.copy()
+            sf = [0.0] * 4
+        else:
+            sf = []
+            for band in SNARE_BANDS:
+                s, e = drum_band_bins(band, n, self.fs)
+                sf.append(np.sum(np.maximum(mag[s:e] - self.prev_s[s:e], 0)))
+            self.prev_s = mag.copy()
+        # spectral centroid (:212-229): frequencies of rfftfreq(2 len - 1), 150 Hz .. 15 kHz
+        freqs = np.fft.rfftfreq(n * 2 - 1, 1 / self.fs)
+        s, e = int(SNARE_BANDS[0][0] * n / (self.fs / 2)), int(SNARE_BANDS[3][1] * n / (self.fs / 2))
+        rel = mag[s:e]
+        cen = np.sum(freqs[s:e] * rel) / np.sum(rel) if np.sum(rel) > 0 else 0
+        for h, v in zip(self.hs, sf):
+            h.append(v)
+        st = [0.0] * 3
+        if len(self.hs[0]) >= 10:
+            st = [adaptive_threshold(self.hs[i], SNARE_MULT[i], self.sens) for i in range(3)]
+        return np.array([*kf, *kt, *sf, *st, cen], dtype=np.float64)
+
+
+def drum_sequence(mags: np.ndarray, fs: float = 48000, sensitivity: float = 1.0) -> np.ndarray:
+    """Features of consecutive magnitude frames of one stream: [F, 14] (DRUM_COLUMNS)."""
+    st = DrumFluxState(fs, sensitivity)
+    return np.stack([st.update(m) for m in mags])

@@ -514,3 +514,62 @@ def test_cfg5_stream_96k_surround():
             agg = np.array(list(st.update(fr, li, tp).values()))
             assert np.all(np.abs(out["meters"][cf][:4] - agg[:4]) < LU_TOL)
             assert abs(out["meters"][cf][4] - agg[4]) < TP_TOL_DB
+
+
+# ---- drum-detection features (omega_drum_features) ----
+# Fluxes are float32 sums as in the reference, but summed in another order (numpy: pairwise; here:
+# per-thread runs + a tree): relative 1e-5 on fluxes and thresholds; the centroid is float64.
+DRUM_RTOL = 1e-5
+
+
+def _drum_close(got, want):
+    scale = np.maximum(np.abs(want), 1e-3 * np.max(np.abs(want), axis=0, keepdims=True) + 1e-12)
+    return np.max(np.abs(got - want) / scale)
+
+
+@pytest.mark.parametrize("name", ["drums_1025", "drums_2049"])
+def test_drum_features_golden(name):
+    """The reference's EnhancedKickDetector / EnhancedSnareDetector outputs (golden) and the oracle's
+    snare thresholds, frame by frame over one stream, from one call."""
+    from omega_gpu.drum_detection import DrumFeatures
+    g = load_golden("drums")
+    mags, ref = g[f"{name}/mags"], g[f"{name}/out"]
+    out = DrumFeatures(FS).process(mags)
+    assert out.shape == (len(mags), 14) and out.dtype == np.float64
+    assert _drum_close(out[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 13]], ref) < DRUM_RTOL
+    assert _drum_close(out, R.drum_sequence(mags)) < DRUM_RTOL
+
+
+def test_drum_features_state_across_calls_and_device_input():
+    """Calls of 1, 7 and the rest of the frames continue one stream (previous frame, histories);
+    device tensors with a padded row stride give the same; reset starts a new stream; a stream's bin
+    count is fixed."""
+    import torch
+    from omega_gpu import Engine, OmegaError
+    from omega_gpu.drum_detection import DrumFeatures
+    mags = load_golden("drums")["drums_1025/mags"]
+    whole = DrumFeatures(FS).process(mags)
+    d = DrumFeatures(FS)
+    parts = np.concatenate([d.process(mags[:1]), d.process(mags[1:8]), d.process(mags[8:])])
+    assert _drum_close(parts, whole) < DRUM_RTOL
+    d.reset()
+    np.testing.assert_array_equal(d.process(mags), whole)
+    eng = Engine(sample_rate=FS)
+    padded = torch.zeros(len(mags), 1040, device="cuda")
+    padded[:, :1025] = torch.from_numpy(mags).cuda()
+    o = eng.drum_features(padded[:, :1025])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(o.cpu().numpy(), whole)
+    with pytest.raises(OmegaError):
+        eng.drum_features(np.zeros((2, 513), np.float32))
+    assert eng.drum_features(np.zeros((0, 1025), np.float32)).shape == (0, 14)
+
+
+def test_drum_features_random_vs_oracle():
+    """Random magnitudes over a long stream (past the 21-deep history, several calls), sensitivity 1.5."""
+    from omega_gpu.drum_detection import DrumFeatures
+    rng = np.random.default_rng(11)
+    mags = np.abs(rng.standard_normal((70, 2049))).astype(np.float32) * np.linspace(2, 0.1, 2049).astype(np.float32)
+    d = DrumFeatures(FS, sensitivity=1.5)
+    got = np.concatenate([d.process(mags[:33]), d.process(mags[33:])])
+    assert _drum_close(got, R.drum_sequence(mags, FS, 1.5)) < DRUM_RTOL

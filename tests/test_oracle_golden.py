@@ -177,3 +177,17 @@ def test_batched(golden):
         r = R.batched_fft(g[f"{name}/x"], n, w)
         np.testing.assert_array_equal(r["magnitude"], g[f"{name}/mag"])
         np.testing.assert_array_equal(r["complex"], g[f"{name}/complex"])
+
+
+# ---- drum-detection features (golden: the reference's detectors themselves) ----
+
+@pytest.mark.parametrize("name", ["drums_1025", "drums_2049"])
+def test_drum_features(name):
+    g = load_golden("drums")
+    mags, ref = g[f"{name}/mags"], g[f"{name}/out"]
+    o = R.drum_sequence(mags)
+    # golden columns: kick sub/body/click flux, sub/body/click threshold, snare fund/body/snap/rattle flux,
+    # spectral centroid (the snare thresholds are not in the reference's return dict)
+    np.testing.assert_array_equal(o[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 13]], ref)
+    # the kick sub band skips the stream's first frame, so its threshold starts one frame after the click band's
+    assert o[9, 5] > 0 and o[9, 3] == 0 and o[10, 3] > 0
