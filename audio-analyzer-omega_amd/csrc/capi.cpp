@@ -798,12 +798,21 @@ int enqueue_batch(omega_ctx* c, const SpectralParams& sp, KWeightParams kp, int 
       HIPC(c, launch_meter_prep(p, c->fork[0]));
       p.parts = 1;
       p.q_done = c->d_kw_done + 1;
-      c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);
       HIPC(c, launch_meter_query(p, c->fork[0]));
+      c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);  // (counted once it is enqueued)
     }
   }
-  if (do_kw && !kw_in_batch) HIPC(c, launch_kweight(W, kp, s));
-  if (grid > 0) HIPC(c, launch_batch(sp, kp, bp, (int)grid, s));
+  {
+    hipError_t le = hipSuccess;
+    if (do_kw && !kw_in_batch) le = launch_kweight(W, kp, s);
+    if (le == hipSuccess && grid > 0) le = launch_batch(sp, kp, bp, (int)grid, s);
+    if (le != hipSuccess) {
+      // the prep kernel already waits for this batch's count: publish it, so that it (and every later
+      // call's target) stays in step with the device counter instead of timing out
+      if (meters) (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
+      return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
+    }
+  }
   for (size_t i = 0; i < mc.size(); ++i) {
     MeterPrepParams p = mc[i];
     p.parts = 2;
