@@ -333,6 +333,21 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   }
   __syncthreads();
   auto is_peak = [&](int q) { return q < 64 * kSpecRfPeakWords && (int)((pkw[q >> 6] >> (q & 63)) & 1ull); };
+  // harmonic suppression (chromagram.py:172-187) as a scatter from the peaks, in the reference's
+  // order per bin (h = 5, 4, 3, 2, float32 multiplies by float32(1/h)): round h scales bin q h of
+  // every peak q inside the chromagram range -- a bin has at most one such q per h, so a round has
+  // no conflicting writes, and the accumulation below reads the suppressed magnitudes directly
+  static_for<0, 4>([&](auto hh) {
+    constexpr int h = 5 - hh;
+    static_for<0, 64 * kSpecRfPeakWords / NTH>([&](auto qq) {
+      const int q = t + NTH * qq;
+      if (is_peak(q)) {
+        const int k = q * h;
+        if (k >= p.c_lo && k < p.c_hi) magc[k] = magc[k] * (1.0f / h);
+      }
+    });
+    __syncthreads();
+  });
   constexpr int kGrp = 20;  // threads per base-class group (12 x 20 = 240 of 256)
   if (t < 12 * kGrp) {
     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
@@ -341,13 +356,7 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
     for (int j = j0 + r; j < j1; j += kGrp) {
       const int i = p.cperm[j];
       const int k = p.c_lo + i;
-      // harmonic suppression (chromagram.py:172-187) in the reference's order (descending h);
-      // float32 multiplies by float32(1/h)
-      float e = magc[k];
-      if (k % 5 == 0 && is_peak(k / 5)) e = e * (1.0f / 5.0f);
-      if (k % 4 == 0 && is_peak(k / 4)) e = e * (1.0f / 4.0f);
-      if (k % 3 == 0 && is_peak(k / 3)) e = e * (1.0f / 3.0f);
-      if (k % 2 == 0 && is_peak(k / 2)) e = e * (1.0f / 2.0f);
+      const float e = magc[k];  // (suppressed above)
       const float4 cw = p.cw4[i];
       const double ed = (double)e;
       acc[0] = fma(ed, (double)cw.x, acc[0]);
