@@ -41,6 +41,7 @@ hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int h
                          hipStream_t s);
 hipError_t launch_combine(const CombineParams& p, hipStream_t s);
 hipError_t launch_drum(const DrumParams& p, hipStream_t s);
+hipError_t launch_post(const PostParams& p, hipStream_t s);
 hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s);
 }  // namespace omega
 
@@ -230,6 +231,7 @@ struct omega_ctx {
   int* d_dlen[2] = {};
   long long* d_dpos[2] = {};
   float* d_dflux = nullptr;
+  PostParams post{};  // omega_post_configure's tables (post.n_bins = 0: not configured)
   int64_t dflux_cap = 0;
   // meter state (double-buffered)
   float* d_hist_l[2] = {};
@@ -1078,6 +1080,99 @@ int omega_drum_features(omega_ctx* c, const float* mag, int64_t n_frames, int32_
   HIPC(c, launch_drum(p, c->stream));
   c->drum_cur = b;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, const uint8_t* bass,
+                         const float* comp_instr, const float* comp_vocal, const float* vocal_sup,
+                         const int32_t* ranges, int32_t p_lo, int32_t p_hi, float p_gamma,
+                         const int32_t* band_start, const int32_t* band_end, const float* band_smooth,
+                         int32_t n_bands) {
+  if (!c) return OMEGA_EINVAL;
+  if (n_bins < 1 || n_bins > kPostMaxBins || n_bands < 0 || n_bands > kPostMaxBands || !curve || !bass ||
+      !comp_instr || !comp_vocal || !vocal_sup || !ranges || (n_bands && (!band_start || !band_end || !band_smooth)))
+    return fail(c, OMEGA_EINVAL, "post configure: bad tables (n_bins %d, n_bands %d)", n_bins, n_bands);
+  if (p_lo < 0 || p_hi < p_lo || p_hi >= n_bins)
+    return fail(c, OMEGA_EINVAL, "post configure: percentile ranks %d, %d outside %d bins", p_lo, p_hi, n_bins);
+  for (int b = 0; b < n_bands; ++b)
+    if (band_start[b] < 0 || band_start[b] >= n_bins || band_end[b] > n_bins || band_end[b] < band_start[b])
+      return fail(c, OMEGA_EINVAL, "post configure: band %d [%d, %d) outside %d bins", b, band_start[b],
+                  band_end[b], n_bins);
+  HIPC(c, hipSetDevice(c->device));
+  PostParams p{};
+  p.T = n_bins;
+  p.nb = n_bands;
+  p.be = ranges[0];
+  p.vs = ranges[1];
+  p.ve = ranges[2];
+  p.hs = ranges[3];
+  p.p_lo = p_lo;
+  p.p_hi = p_hi;
+  p.p_g = p_gamma;
+  auto up = [&](auto** d, const auto* h, size_t n) {
+    int e = dalloc(c, d, n);
+    if (!e && n) {
+      const hipError_t he = hipMemcpy(*d, h, n * sizeof(**d), hipMemcpyHostToDevice);
+      if (he != hipSuccess) e = fail(c, OMEGA_EHIP, "post configure: %s", hipGetErrorString(he));
+    }
+    return e;
+  };
+  double* dc = nullptr;
+  unsigned char* db = nullptr;
+  float *d0 = nullptr, *d1 = nullptr, *dv = nullptr, *dsf = nullptr;
+  int *dbs = nullptr, *dbe = nullptr;
+  int e = up(&dc, curve, (size_t)n_bins);
+  if (!e) e = up(&db, bass, (size_t)n_bins);
+  if (!e) e = up(&d0, comp_instr, (size_t)n_bins);
+  if (!e) e = up(&d1, comp_vocal, (size_t)n_bins);
+  if (!e) e = up(&dv, vocal_sup, (size_t)n_bins);
+  if (!e) e = up(&dbs, band_start, (size_t)n_bands);
+  if (!e) e = up(&dbe, band_end, (size_t)n_bands);
+  if (!e) e = up(&dsf, band_smooth, (size_t)n_bands * 2);
+  if (!e) e = dalloc(c, &p.prev, (size_t)std::max(n_bands, 1));
+  if (!e) e = dalloc(c, &p.has_prev, 1);
+  if (e) return e;
+  p.curve = dc;
+  p.bass = db;
+  p.comp[0] = d0;
+  p.comp[1] = d1;
+  p.vsup = dv;
+  p.bs = dbs;
+  p.bend = dbe;
+  p.sf = dsf;
+  c->post = p;
+  return omega_post_reset(c);
+}
+
+int omega_post_reset(omega_ctx* c) {
+  if (!c) return OMEGA_EINVAL;
+  if (!c->post.T) return 0;
+  HIPC(c, hipSetDevice(c->device));
+  HIPC(c, hipMemsetAsync(c->post.has_prev, 0, sizeof(int), c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int64_t stride, int32_t flags,
+                       float bass_boost, float* spectrum_out, float* bands_out, int32_t* content_out) {
+  if (!c) return OMEGA_EINVAL;
+  if (!c->post.T) return fail(c, OMEGA_EINVAL, "post process: omega_post_configure first");
+  if (n_frames < 0 || stride < c->post.T || !spectra || !spectrum_out || (c->post.nb && !bands_out) ||
+      n_frames > 0x7FFFFFFF)
+    return fail(c, OMEGA_EINVAL, "post process: bad layout (n %lld, stride %lld, %d bins)", (long long)n_frames,
+                (long long)stride, c->post.T);
+  if (n_frames == 0) return 0;
+  HIPC(c, hipSetDevice(c->device));
+  PostParams p = c->post;
+  p.in = spectra;
+  p.n = n_frames;
+  p.stride = stride;
+  p.flags = flags;
+  p.bass_boost = bass_boost;
+  p.spec_out = spectrum_out;
+  p.band_out = bands_out;
+  p.content_out = content_out;
+  HIPC(c, launch_post(p, c->stream));
   return 0;
 }
 

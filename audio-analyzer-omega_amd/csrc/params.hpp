@@ -236,6 +236,33 @@ constexpr int kDrumBands = 7;
 constexpr int kDrumHist = 21;
 constexpr int kDrumCols = 14;
 
+// App spectrum post-processing (post.hip): per-bin tables from the host.
+constexpr int kPostMaxBins = 2048;
+constexpr int kPostMaxBands = 1024;
+struct PostParams {
+  const float* in;  // [n, stride] combined spectra
+  int64_t n, stride;
+  int T;
+  const double* curve;         // [T] equal-loudness curve by position
+  const unsigned char* bass;   // [T] combine frequency < 250 Hz
+  const float* comp[2];        // [T] frequency compensation: [0] instrumental / bass-heavy, [1] vocal
+  const float* vsup;           // [T] vocal-suppression factor (1 outside 800-4000 Hz)
+  int be, vs, ve, hs;          // content ranges [0, be), [vs, ve), [hs, T)
+  int p_lo, p_hi;              // 98th percentile: sorted ranks and float32 gamma
+  float p_g;
+  const int* bs;               // [nb] band starts / ends
+  const int* bend;
+  const float* sf;             // [nb] EMA factor
+  int nb;
+  int flags;                   // OMEGA_POST_* bits
+  float bass_boost;
+  float* spec_out;             // [n, T]
+  float* band_out;             // [n, nb]
+  int* content_out;            // [n]
+  float* prev;                 // [nb] EMA state
+  int* has_prev;
+};
+
 struct DrumParams {
   const float* mag;
   int64_t n, stride;

@@ -1,0 +1,165 @@
+// App spectrum post-processing after the path: what
+// omega4_main.ProfessionalLiveAudioAnalyzer does to the combined spectrum of every frame
+//   process_multi_resolution_fft  omega4_main.py:748-752  equal-loudness curve by position, bass boost
+//   update_content_type           :805-840   bass / vocal / high energy ratios -> content type
+//   process_audio_spectrum        :991-997   98th-percentile normalisation (x 0.8)
+//   apply_frequency_compensation  :855-926   content-dependent per-bin factors, vocal suppression
+//                                 :1004-1005 optional max normalisation
+//                                 :1011-1036 band means, sqrt, clamp to [0, 1]
+//                                 :1041-1056 frequency-dependent band EMA across frames
+// in float32 as numpy runs them (in-place multiplies by weak Python scalars; the percentile's virtual
+// index and gamma in float32).
+//   post_frame_kernel: one 256-thread workgroup per frame (independent frames).
+//   post_ema_kernel: one workgroup, one thread per band, the frames in order (the EMA recurrence).
+#include "fft.hpp"
+#include "params.hpp"
+
+namespace omega {
+
+namespace {
+
+constexpr int kPostThreads = 256;
+
+template <class T, class Op>
+__device__ __forceinline__ T block_reduce(T v, T* red, int t, Op op) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+  __syncthreads();
+  if ((t & 63) == 0) red[t >> 6] = v;
+  __syncthreads();
+  T r = red[0];
+#pragma unroll
+  for (int w = 1; w < kPostThreads / 64; ++w) r = op(r, red[w]);
+  return r;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) {
+  __shared__ float s[kPostMaxBins];
+  __shared__ double redd[kPostThreads / 64];
+  __shared__ float redf[kPostThreads / 64];
+  __shared__ float pv[2];
+  const int t = threadIdx.x, T = p.T;
+  const int64_t f = blockIdx.x;
+  const float* in = p.in + f * p.stride;
+  // 1) equal-loudness curve (float64 product rounded into the float32 array) and bass boost
+  for (int i = t; i < T; i += kPostThreads) {
+    float v = in[i];
+    if (p.flags & 1) {
+      v = (float)((double)v * p.curve[i]);
+      if (p.bass[i]) v = v * p.bass_boost;
+    }
+    s[i] = v;
+  }
+  __syncthreads();
+  // 2) content type from the range means (omega4_main.py:805-840; voice detection is not on the path)
+  auto dsum = [](double a, double b) { return a + b; };
+  auto fmx = [](float a, float b) { return fmaxf(a, b); };
+  double sb = 0.0, sv = 0.0, sh = 0.0, st = 0.0;
+  float mx = -INFINITY;
+  for (int i = t; i < T; i += kPostThreads) {
+    const double v = s[i];
+    if (i < p.be) sb += v;
+    if (i >= p.vs && i < p.ve) sv += v;
+    if (i >= p.hs) sh += v;
+    st += v;
+    mx = fmaxf(mx, s[i]);
+  }
+  sb = block_reduce(sb, redd, t, dsum);
+  sv = block_reduce(sv, redd, t, dsum);
+  sh = block_reduce(sh, redd, t, dsum);
+  st = block_reduce(st, redd, t, dsum);
+  mx = block_reduce(mx, redf, t, fmx);
+  const float eb = p.be < T ? (float)(sb / p.be) : 0.f;
+  const float ev = p.ve < T ? (float)(sv / (p.ve - p.vs)) : 0.f;
+  const float eh = p.hs < T ? (float)(sh / (T - p.hs)) : 0.f;
+  const float et = (float)(st / T);
+  int content = 0;  // 0 instrumental, 1 vocal, 2 bass-heavy
+  if (et > 0.f) {
+    const float br = eb / et, vr = ev / et;
+    if (br > 0.6f)
+      content = 2;
+    else if ((vr > 0.4f && br < 0.4f) || (vr > 0.3f && eh < ev * 0.5f))
+      content = 1;
+  }
+  // 3) 98th percentile (numpy 'linear', float32): the values of sorted ranks p_lo and p_hi
+  if (mx > 0.f) {
+    for (int i = t; i < T; i += kPostThreads) {
+      const float v = s[i];
+      int r = 0;
+      for (int j = 0; j < T; ++j) {
+        const float u = s[j];
+        r += (u < v) || (u == v && j < i);
+      }
+      if (r == p.p_lo) pv[0] = v;
+      if (r == p.p_hi) pv[1] = v;
+    }
+    __syncthreads();
+    const float a = pv[0], b = pv[1], d = b - a;
+    // numpy _lerp, no contraction
+    const float ref = p.p_g >= 0.5f ? __fsub_rn(b, __fmul_rn(d, 1.0f - p.p_g)) : __fadd_rn(a, __fmul_rn(d, p.p_g));
+    if (ref > 0.f)
+      for (int i = t; i < T; i += kPostThreads) s[i] = __fmul_rn(__fdiv_rn(s[i], ref), 0.8f);
+  }
+  // 4) frequency compensation (factors by position) and 5) optional max normalisation
+  const float* comp = p.comp[content == 1 ? 1 : 0];
+  if (p.flags & 2)
+    for (int i = t; i < T; i += kPostThreads) s[i] = s[i] * comp[i] * p.vsup[i];
+  __syncthreads();
+  if (p.flags & 4) {
+    float m = -INFINITY;
+    for (int i = t; i < T; i += kPostThreads) m = fmaxf(m, s[i]);
+    m = block_reduce(m, redf, t, fmx);
+    if (m > 0.f)
+      for (int i = t; i < T; i += kPostThreads) s[i] = __fdiv_rn(s[i], m);
+    __syncthreads();
+  }
+  for (int i = t; i < T; i += kPostThreads) p.spec_out[f * T + i] = s[i];
+  // 6) band means -> sqrt -> clamp (before the EMA)
+  for (int b = t; b < p.nb; b += kPostThreads) {
+    const int lo = p.bs[b], hi = p.bend[b];
+    float v;
+    if (hi > lo) {
+      double a = 0.0;
+      for (int i = lo; i < hi; ++i) a += s[i];
+      v = (float)(a / (hi - lo));
+    } else {
+      v = s[lo];
+    }
+    if (v > 0.f) v = fminf(__fsqrt_rn(v), 1.0f);
+    p.band_out[f * p.nb + b] = v;
+  }
+  if (t == 0 && p.content_out) p.content_out[f] = content;
+}
+
+// band_out holds the clamped band values of the n frames; the EMA runs over them in frame order
+__global__ __launch_bounds__(kPostMaxBands) void post_ema_kernel(PostParams p) {
+  const int b = threadIdx.x;
+  const bool had = *p.has_prev != 0;
+  __syncthreads();
+  if (b < p.nb) {
+    const float sf = p.sf[b], sf1 = p.sf[p.nb + b];  // float32(f), float32(1 - f)
+    float prev = had ? p.prev[b] : 0.f;
+    bool have = had;
+    for (int64_t f = 0; f < p.n; ++f) {
+      float v = p.band_out[f * p.nb + b];
+      if ((p.flags & 8) && have) v = __fadd_rn(__fmul_rn(prev, sf), __fmul_rn(v, sf1));
+      p.band_out[f * p.nb + b] = v;
+      prev = v;
+      have = true;
+    }
+    p.prev[b] = prev;
+  }
+  if (b == 0 && p.n > 0) *p.has_prev = 1;
+}
+
+hipError_t launch_post(const PostParams& p, hipStream_t s) {
+  if (p.T < 1 || p.T > kPostMaxBins || p.nb < 0 || p.nb > kPostMaxBands) return hipErrorInvalidValue;
+  if (p.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(post_frame_kernel, dim3((unsigned)p.n), dim3(kPostThreads), 0, s, p);
+  hipLaunchKernelGGL(post_ema_kernel, dim3(1), dim3(kPostMaxBands), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace omega

@@ -82,6 +82,11 @@ EXPORTS = {
     "omega_drum_features": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int64, C.c_double,
                                       C.c_void_p, C.c_int]),
     "omega_drum_reset": (C.c_int, [C.c_void_p]),
+    "omega_post_configure": (C.c_int, [C.c_void_p, C.c_int32] + [C.c_void_p] * 6 + [C.c_int32, C.c_int32, C.c_float]
+                             + [C.c_void_p] * 3 + [C.c_int32]),
+    "omega_post_process": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int32, C.c_float,
+                                     C.c_void_p, C.c_void_p, C.c_void_p]),
+    "omega_post_reset": (C.c_int, [C.c_void_p]),
     "omega_rfft": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                              C.c_int]),
 }

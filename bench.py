@@ -154,6 +154,34 @@ def drums_line(dev, reps=20, n=4096, bins=1025):
                          "bytes_per_frame": bpf}}
 
 
+def post_line(dev, reps=20, n=4096, bins=512):
+    """SURVEY.md §8(f) row 2 (the app's spectrum post-processing): one call over n consecutive
+    combined spectra of one stream (equal-loudness, content type, p98 normalisation, compensation,
+    band means + EMA), device-resident. Bytes per frame: the spectrum in, spectrum + bands + content out."""
+    from omega_gpu.app_post import SpectrumPostProcessor
+    rng = np.random.default_rng(6)
+    x = torch.from_numpy(rng.random((n, bins)).astype(np.float32)).to(dev)
+    pp = SpectrumPostProcessor(np.linspace(20, 20000, bins), device=dev.index or 0)
+    for _ in range(3):
+        pp.process(x)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        pp.process(x)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    bpf = 4 * (2 * bins + pp.n_bands + 1)
+    gbs = n * bpf / (ms * 1e-3) / 1e9
+    return {"workload": f"app post-processing: {n} consecutive combined spectra x {bins} bins of one stream "
+                        f"({pp.n_bands} bands)",
+            "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_call": ms,
+            "roofline": {"bound": "hbm", "kernel": "post_frame_kernel + post_ema_kernel", "achieved": gbs,
+                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
+                         "bytes_per_frame": bpf}}
+
+
 def cfg3_input(n, m):
     """BASELINE cfg3 synthetic frames (same generator as oracle/signals.cfg3_batch): even frames a
     0.5-amplitude C-major triad, odd frames 0.1 N(0,1) (seed 1234)."""
@@ -351,6 +379,7 @@ def main():
         if world == 1 and not a.no_cfg3:
             line["cfg3"] = cfg3_line(dev)
             line["drums"] = drums_line(dev)
+            line["app_post"] = post_line(dev)
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

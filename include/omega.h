@@ -203,6 +203,34 @@ int omega_rfft(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t win
 int omega_drum_features(omega_ctx* ctx, const float* mag, int64_t n_frames, int32_t n_bins, int64_t mag_stride,
                         double sensitivity, double* out, int mem);
 int omega_drum_reset(omega_ctx* ctx);
+
+/* App spectrum post-processing of combined spectra -- replaces the per-frame
+ * part of omega4_main.ProfessionalLiveAudioAnalyzer after combine_results_optimized:
+ * process_multi_resolution_fft :748-752 (equal-loudness curve, bass boost), update_content_type
+ * :805-840, process_audio_spectrum :991-1056 (98th-percentile normalisation,
+ * apply_frequency_compensation :855-926, optional max normalisation, band means -> sqrt -> clamp,
+ * frequency-dependent band EMA). omega_post_configure uploads the host-built tables (host memory):
+ * curve[T] equal-loudness by position, bass[T] (combine frequency < 250 Hz), comp_instr / comp_vocal
+ * [T] compensation factors, vocal_sup[T], ranges {bass_end, vocal_start, vocal_end, high_start},
+ * the percentile's sorted ranks and float32 gamma, bands [n_bands] (start, end) already truncated
+ * as the reference's loop does, band_smooth[2 * n_bands] = float32(f), float32(1 - f).
+ * omega_post_process (device memory only): n_frames spectra at row stride `stride` -> spectrum_out
+ * [n, T], bands_out [n, n_bands] (after the EMA, which runs across frames in order and across calls),
+ * content_out [n] (0 instrumental, 1 vocal, 2 bass-heavy; may be NULL). flags: OMEGA_POST_*. */
+enum {
+  OMEGA_POST_PSYCHO = 1,      /* equal-loudness curve + bass boost */
+  OMEGA_POST_FREQ_COMP = 2,   /* apply_frequency_compensation */
+  OMEGA_POST_NORMALIZE = 4,   /* final max normalisation */
+  OMEGA_POST_SMOOTH = 8       /* band EMA */
+};
+int omega_post_configure(omega_ctx* ctx, int32_t n_bins, const double* curve, const uint8_t* bass,
+                         const float* comp_instr, const float* comp_vocal, const float* vocal_sup,
+                         const int32_t* ranges, int32_t p_lo, int32_t p_hi, float p_gamma,
+                         const int32_t* band_start, const int32_t* band_end, const float* band_smooth,
+                         int32_t n_bands);
+int omega_post_process(omega_ctx* ctx, const float* spectra, int64_t n_frames, int64_t stride, int32_t flags,
+                       float bass_boost, float* spectrum_out, float* bands_out, int32_t* content_out);
+int omega_post_reset(omega_ctx* ctx);
 int omega_spectra(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t window, omega_bands* bands,
                   float* bands_out, double* chroma_out, float* mag_out, int mem);
 

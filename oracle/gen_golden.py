@@ -249,6 +249,107 @@ def gen_drums(R):
     np.savez_compressed(os.path.join(OUT, "drums.npz"), **d)
 
 
+def _import_app():
+    """omega4_main (the app module): it needs a more permissive pygame stub than the panel modules --
+    module attributes that are classes whose attributes are classes (type annotations, pygame.Rect)."""
+    class _Meta(type):
+        def __getattr__(cls, n):
+            return _Any
+
+    class _Any(metaclass=_Meta):
+        def __init__(self, *a, **k):
+            pass
+
+        def __call__(self, *a, **k):
+            return _Any()
+
+        def __getattr__(self, n):
+            return _Any()
+
+    for n in ("pygame", "pygame.gfxdraw", "pygame.font", "pygame.mixer", "pygame.locals", "pygame.surfarray",
+              "pygame.draw"):
+        m = types.ModuleType(n)
+        m.__getattr__ = lambda name: _Any
+        m.__path__ = []
+        sys.modules[n] = m
+    import omega4_main
+    return omega4_main
+
+
+class _Stop(Exception):
+    pass
+
+
+def gen_post(R):
+    """The app's own per-frame post-processing, run through the reference's methods on a stand-in
+    analyzer object: process_audio_spectrum (omega4_main.py:928-1056) calling the real
+    process_multi_resolution_fft / update_content_type / apply_frequency_compensation, with the real
+    MultiResolutionFFT behind a recorder of its combined spectrum (the input of the GPU path) and a drum
+    detector that stops the frame once spectrum and band values are final (:1069)."""
+    M = _import_app()
+    A = M.ProfessionalLiveAudioAnalyzer
+    d = {"versions": VERSIONS}
+    rng = np.random.default_rng(11)
+    for name, kw in (("default", {}), ("vocal_supp_norm", {"vocal_suppression": 0.4, "normalization_enabled": True}),
+                     ("flat", {"psychoacoustic_enabled": False, "freq_compensation_enabled": False,
+                               "smoothing_enabled": False})):
+        app = SimpleNamespace()
+        for m in ("process_multi_resolution_fft", "update_content_type", "apply_frequency_compensation",
+                  "auto_adjust_gain", "_create_equal_loudness_curve"):
+            setattr(app, m, types.MethodType(getattr(A, m), app))
+        mf = R.MultiResolutionFFT(FS)
+        rec = []
+
+        class Rec:
+            def process_audio_chunk(self, x, apply_weighting=True):
+                return mf.process_audio_chunk(x, apply_weighting)
+
+            def combine_results_optimized(self, res, target_bins=1024):
+                s, f = mf.combine_results_optimized(res, target_bins)
+                rec.append((s.copy(), f.copy()))
+                return s, f
+
+        class Drums:
+            def process_audio(self, spectrum, bands):
+                raise _Stop(spectrum.copy(), np.array(bands, dtype=np.float64))
+
+        prof = SimpleNamespace(profiler=SimpleNamespace(update_audio_latency=lambda *a: None))
+        bf = SimpleNamespace(prepare_batch=lambda *a, **k: 0, process_batch=lambda: 0, distribute_results=lambda: {})
+        app.__dict__.update(dict(
+            bars=512, freqs=np.fft.rfftfreq(M.FFT_SIZE_BASE, 1 / M.SAMPLE_RATE), multi_fft=Rec(),
+            psychoacoustic_enabled=True, freq_compensation_enabled=True, normalization_enabled=False,
+            smoothing_enabled=True, vocal_suppression=0.0, psycho_bass_boost=1.5, auto_gain_enabled=False,
+            voice_active=False, voice_confidence=0, adaptive_allocation_enabled=False,
+            current_content_type="instrumental", current_allocation=0.7, performance_profiler=prof,
+            batched_fft=bf, transient_events=[], last_transient_time=0.0, drum_detector=Drums(),
+            buffer_pos=M.FFT_SIZE_BASE, ring_buffer=np.zeros(M.FFT_SIZE_BASE * 4, np.float32)))
+        app.band_indices = R.PrecomputedFrequencyMapper(M.SAMPLE_RATE, M.FFT_SIZE_BASE, 512).mapping.band_indices
+        app.equal_loudness_curve = app._create_equal_loudness_curve()
+        app.__dict__.update(kw)
+        t = np.arange(M.FFT_SIZE_BASE) / FS
+        comb, spec, bands, content = [], [], [], []
+        for i in range(24):
+            # alternate bass-heavy, vocal-range and broadband frames so every content branch is taken
+            f0 = (55.0, 700.0, 2500.0)[i % 3] * (1 + 0.05 * i)
+            x = (0.4 * np.sin(2 * np.pi * f0 * t) + 0.2 * np.sin(2 * np.pi * 3.1 * f0 * t)
+                 + 0.02 * (i % 4) * rng.standard_normal(len(t))).astype(np.float32)
+            app.ring_buffer[:M.FFT_SIZE_BASE] = x
+            try:
+                A.process_audio_spectrum(app)
+                raise RuntimeError("process_audio_spectrum returned before drum detection")
+            except _Stop as e:
+                spec.append(e.args[0])
+                bands.append(e.args[1])
+            comb.append(rec[-1][0])
+            content.append(("instrumental", "vocal", "bass_heavy").index(app.current_content_type))
+        d[f"{name}/combined"] = np.stack(comb).astype(np.float32)
+        d[f"{name}/freqs"] = rec[-1][1]
+        d[f"{name}/spectrum"] = np.stack(spec)
+        d[f"{name}/bands"] = np.stack(bands)
+        d[f"{name}/content"] = np.array(content, np.int32)
+    np.savez_compressed(os.path.join(OUT, "app_post.npz"), **d)
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference not present: golden vectors can only be generated in the build container")

@@ -661,3 +661,125 @@ def drum_sequence(mags: np.ndarray, fs: float = 48000, sensitivity: float = 1.0)
     """Features of consecutive magnitude frames of one stream: [F, 14] (DRUM_COLUMNS)."""
     st = DrumFluxState(fs, sensitivity)
     return np.stack([st.update(m) for m in mags])
+
+
+# ---- App spectrum post-processing (SURVEY.md §8(f) row 2): omega4_main.ProfessionalLiveAudioAnalyzer,
+# FFT_SIZE_BASE = 2048 and bars = 512 there. float32 arrays throughout, in-place multiplies by Python
+# scalars (NEP 50 weak scalars -> float32), as the reference runs them.
+
+def app_equal_loudness(fs: float = 48000, fft_base: int = 2048) -> np.ndarray:
+    """_create_equal_loudness_curve omega4_main.py:617-644 (float64, indexed by position)."""
+    f = np.fft.rfftfreq(fft_base, 1 / fs)[:fft_base // 2 + 1]
+    c = np.ones_like(f)
+    c[f < 200] = 1 + (200 - f[f < 200]) / 50
+    for lo, hi, g in ((500, 2000, 0.85), (2000, 5000, 1.05)):
+        c[(f > lo) & (f < hi)] *= g
+    c[f > 6000] *= 0.5
+    c[f > 10000] *= 0.2
+    return c
+
+
+def app_content_type(s: np.ndarray, fs: float = 48000) -> int:
+    """update_content_type :805-840 without voice detection: 0 instrumental, 1 vocal, 2 bass-heavy."""
+    n = len(s)
+    w = fs / (2 * n)
+    be, vs, ve, hs = int(250 / w), int(200 / w), int(4000 / w), int(6000 / w)
+    eb = np.mean(s[:be]) if be < n else 0
+    ev = np.mean(s[vs:ve]) if ve < n else 0
+    eh = np.mean(s[hs:]) if hs < n else 0
+    et = np.mean(s)
+    if not et > 0:
+        return 0
+    br, vr = eb / et, ev / et
+    if br > 0.6:
+        return 2
+    if (vr > 0.4 and br < 0.4) or (vr > 0.3 and eh < ev * 0.5):
+        return 1
+    return 0
+
+
+def app_compensation(s: np.ndarray, f: np.ndarray, content: int, vocal_suppression: float = 0.0) -> np.ndarray:
+    """apply_frequency_compensation :855-926 (freqs = the base FFT's, by position)."""
+    out = s.copy()
+    first = ((0.15, 0.2, 0.6, 1.5) if content == 1 else (0.8, 1.0, 1.1, 0.85))
+    edges = (-np.inf, 60, 250, 500, 2000, 6000, 10000, np.inf)
+    for (lo, hi), g in zip(zip(edges[:-1], edges[1:]), first + (1.2, 0.8, 0.3)):
+        m = (f < hi) if lo == -np.inf else ((f >= lo) & (f < hi))
+        out[m] *= g
+    if vocal_suppression > 0:
+        out[(f >= 800) & (f < 4000)] *= (1.0 - vocal_suppression * 0.5)
+    return out
+
+
+def app_band_table(fs: float = 48000, fft_base: int = 2048, bars: int = 512, n_bins: int = 512):
+    """PrecomputedFrequencyMapper band_indices (freq_mapper.py:83-124) as the spectrum loop uses them
+    (:1011-1036: stop at the first band ending past the spectrum, then [:bars]) and the EMA factor by the
+    band's start frequency (:1044-1052)."""
+    width = fs / fft_base
+    mel = np.linspace(2595 * np.log10(1 + 20 / 700), 2595 * np.log10(1 + 20000 / 700), bars + 1)
+    fp = [700 * (10 ** (m / 2595) - 1) for m in mel]
+    fp[0], fp[-1] = max(20, fp[0]), min(20000, fp[-1])
+    bands = []
+    for i in range(min(bars, len(fp) - 1)):
+        s, e = int(fp[i] / width), int(fp[i + 1] / width)
+        e = s + 1 if e <= s else e
+        s = max(0, min(s, fft_base // 2))
+        bands.append((s, max(s + 1, min(e, fft_base // 2 + 1))))
+    keep = []
+    for s, e in bands:
+        if e > n_bins:
+            break
+        keep.append((s, e))
+    keep = keep[:bars]
+    sf = [0.6 if s * fs / fft_base < 250 else (0.75 if s * fs / fft_base < 2000 else 0.85) for s, _ in keep]
+    return keep, sf
+
+
+class AppPostState:
+    """process_multi_resolution_fft :748-752 + process_audio_spectrum :991-1056 for one stream."""
+
+    def __init__(self, comb_freqs, fs=48000, fft_base=2048, bars=512, psycho=True, bass_boost=1.5,
+                 freq_comp=True, normalization=False, smoothing=True, vocal_suppression=0.0):
+        self.cf, self.fs, self.fft_base, self.bars = np.asarray(comb_freqs), fs, fft_base, bars
+        self.psycho, self.boost, self.freq_comp = psycho, bass_boost, freq_comp
+        self.norm, self.smooth, self.vs = normalization, smoothing, vocal_suppression
+        self.curve = app_equal_loudness(fs, fft_base)
+        self.freqs = np.fft.rfftfreq(fft_base, 1 / fs)
+        self.prev = None
+
+    def update(self, comb: np.ndarray):
+        s = np.array(comb, dtype=np.float32)
+        n = len(s)
+        if self.psycho:
+            s *= self.curve[:n]
+            s[self.cf < 250] *= self.boost
+        content = app_content_type(s, self.fs)
+        if np.max(s) > 0:
+            ref = np.percentile(s, 98)
+            if ref > 0:
+                s = s / ref * 0.8
+        if self.freq_comp:
+            s = app_compensation(s, self.freqs[:n], content, self.vs)
+        if self.norm and np.max(s) > 0:
+            s = s / np.max(s)
+        bands, sf = app_band_table(self.fs, self.fft_base, self.bars, n)
+        vals = []
+        for a, b in bands:
+            v = np.mean(s[a:b]) if b > a else s[a]
+            if v > 0:
+                v = max(0, min(1, np.sqrt(v)))
+            vals.append(v)
+        vals = np.array(vals)
+        if self.smooth and self.prev is not None:
+            for i, f in enumerate(sf):
+                vals[i] = self.prev[i] * f + vals[i] * (1 - f)
+        self.prev = vals.copy()
+        return s, vals, content
+
+
+def app_post_sequence(combined: np.ndarray, comb_freqs, **kw):
+    """[F, T] combined spectra of one stream -> (spectrum [F, T], bands [F, nb], content [F])."""
+    st = AppPostState(comb_freqs, **kw)
+    out = [st.update(c) for c in combined]
+    return (np.stack([o[0] for o in out]), np.stack([o[1] for o in out]).astype(np.float64),
+            np.array([o[2] for o in out], np.int32))

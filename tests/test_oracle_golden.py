@@ -191,3 +191,19 @@ def test_drum_features(name):
     np.testing.assert_array_equal(o[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 13]], ref)
     # the kick sub band skips the stream's first frame, so its threshold starts one frame after the click band's
     assert o[9, 5] > 0 and o[9, 3] == 0 and o[10, 3] > 0
+
+
+POST_CFG = {"default": {}, "vocal_supp_norm": dict(vocal_suppression=0.4, normalization=True),
+            "flat": dict(psycho=False, freq_comp=False, smoothing=False)}
+
+
+@pytest.mark.parametrize("name", sorted(POST_CFG))
+def test_app_post(name):
+    """The app's own process_audio_spectrum (run on the reference's methods, gen_golden.gen_post) over
+    24 frames of one stream: the restatement is bit-exact on spectrum, band values and content type."""
+    g = load_golden("app_post")
+    s, b, c = R.app_post_sequence(g[f"{name}/combined"], g[f"{name}/freqs"], **POST_CFG[name])
+    np.testing.assert_array_equal(s, g[f"{name}/spectrum"])
+    np.testing.assert_array_equal(b, g[f"{name}/bands"])
+    np.testing.assert_array_equal(c, g[f"{name}/content"])
+    assert set(c.tolist()) >= {1, 2}
