@@ -7,10 +7,17 @@ across ranks (weak scaling) and each step's per-frame outputs are gathered to ra
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, this process starts the N rank processes
+itself (before touching any GPU) and exits with their status. Every run also measures cfg4's per-GPU
+shard (4096 stereo frames per GPU = BASELINE cfg4's 32768 at N = 8) as the `cfg4` object.
 """
 import argparse
+import importlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,18 +31,20 @@ import torch  # noqa: E402
 FS = 48000
 W = 16384
 FRAMES = 256          # stereo frames per GPU (BASELINE cfg2)
+FRAMES_CFG4 = 4096    # stereo frames per GPU (BASELINE cfg4: 32768 over 8 GPUs)
 C = 2
 T = 512
-PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
+PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector peak
 PEAK_HBM_GBS = 8000.0
 # SURVEY.md §8(d), per channel-frame (cfg2)
 FLOP_TP = 2.5 * W * np.log2(W) + 2.5 * 4 * W * np.log2(4 * W) + 8 * W          # 3.33 MFLOP (reference algorithm)
 FLOP_FFT = sum(2.5 * n * np.log2(n) + 3.5 * n for n in (16384, 8192, 4096, 1024))  # 1.09 MFLOP
 FLOP_KW = 4 * (W + 18) * 9 + 5 * W                                                 # 0.67 MFLOP
 BYTES_CF = 4 * W + 4 * (T + 2)                                                     # 67,592 B
+METRIC = "audio frames/sec (multi-res FFT + LUFS + TruePeak) at 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -45,8 +54,15 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="processes of the all-cores CPU baseline (the GPU box's CPU share is 16)")
-    ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 (HBM-roofline) line")
-    return ap.parse_args()
+    ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 / drums / app_post lines")
+    ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 per-GPU-shard line")
+    ap.add_argument("--cfg4-steps", type=int, default=20)
+    # test hooks (tests/test_bench_launch.py): a stand-in compute backend on the CPU over gloo, a
+    # smaller per-rank batch, and rank 0 dumping the last gathered blocks
+    ap.add_argument("--standin", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--frames", type=int, default=FRAMES, help=argparse.SUPPRESS)
+    ap.add_argument("--dump", default=None, help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
 
 def cfg2_input(frames=FRAMES, w=W, seed_l=0, seed_r=1):
@@ -60,6 +76,141 @@ def cfg2_input(frames=FRAMES, w=W, seed_l=0, seed_r=1):
     right = (0.25 * np.sin(2 * np.pi * 997 * t)).astype(np.float32) + \
         (0.05 * np.random.default_rng(seed_r).standard_normal(n)).astype(np.float32)
     return np.stack([left.reshape(frames, w), right.reshape(frames, w)], axis=1).astype(np.float32)
+
+
+# ---------------------------------------------------------------------------------------------
+# rank launcher
+# ---------------------------------------------------------------------------------------------
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv):
+    """Start n rank processes of this script (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* as
+    torch.distributed.run sets them, rendezvous on 127.0.0.1) and return the first non-zero exit
+    status, or 0. Called before this process touches any GPU; a failing rank stops the others."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---------------------------------------------------------------------------------------------
+# compute backends: the product path (libomega on this rank's GPU) -- tests inject a CPU stand-in
+# ---------------------------------------------------------------------------------------------
+
+
+class DeviceBackend:
+    """libomega.so on this rank's MI355X through the omega_gpu Engine (the product path)."""
+
+    dist_backend = "nccl"
+
+    def __init__(self, local):
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
+        self.eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=T, n_channels=C, device=local)
+
+    def input(self, frames, seed_l, seed_r):
+        return torch.from_numpy(cfg2_input(frames, W, seed_l=seed_l, seed_r=seed_r)).to(self.dev)
+
+    def alloc(self, layout):
+        return layout.alloc(self.dev)
+
+    def reset(self):
+        self.eng.reset_meters()
+
+    def process(self, x, frames, out):
+        self.eng.process_frames(x, frames, C * W, W, meters=True, out=out)
+
+    def sync(self):
+        torch.cuda.synchronize(self.dev)
+
+
+def measure(be, rank, world, frames, steps, warmup, gather, seed_base=None):
+    """Time `steps` passes of the hot path over this rank's batch of `frames` stereo frames (after
+    `warmup` untimed ones), each step's packed outputs gathered to rank 0 asynchronously
+    (double-buffered: step i waits only for the gather of step i - 2). Returns (max-over-ranks
+    seconds, rank 0's last gathered blocks or None, layout)."""
+    from omega_gpu import dist as D
+    sb = 2 * rank if seed_base is None else seed_base
+    x = be.input(frames, sb, sb + 1)
+    ncf = frames * C
+    lay = D.PackedLayout(ncf, T)
+    bufs = [be.alloc(lay) for _ in range(2)]
+    views = [lay.views(b) for b in bufs]
+    recv = [[be.alloc(lay) for _ in range(world)] if rank == 0 else None for _ in range(2)]
+    pending = [None, None]
+    be.reset()
+
+    def step(i):
+        b = i % 2
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
+        be.process(x, frames, views[b])
+        if gather:
+            pending[b] = D.gather_to_root(bufs[b], recv[b], async_op=True)
+
+    def drain():
+        for k in range(2):
+            if pending[k] is not None:
+                pending[k].wait()
+                pending[k] = None
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        be.sync()
+
+    for i in range(warmup):
+        step(i)
+    drain()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(warmup, warmup + steps):
+        step(i)
+    drain()
+    be.sync()
+    t1 = time.perf_counter()
+    barrier()
+    dt = t1 - t0
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([dt], dtype=torch.float64, device=getattr(be, "dev", None))
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    last = (warmup + steps - 1) % 2
+    got = recv[last] if (gather and rank == 0) else None
+    return dt, got, lay
+
+
+# ---------------------------------------------------------------------------------------------
+# per-kernel timings and the other BASELINE configs (rank 0 / N = 1 lines)
+# ---------------------------------------------------------------------------------------------
 
 
 def kernel_time_ms(eng, xd, reps=20):
@@ -118,11 +269,12 @@ def cfg3_line(dev, reps=20):
     ms = s.elapsed_time(e) / reps
     bpf = 4 * m + 4 * (512 + 12)
     gbs = n * bpf / (ms * 1e-3) / 1e9
+    traffic, src = kernel_traffic("cfg3")
     return {"workload": "cfg3: 4096 mono frames x 8192, Hann rfft -> 512 log bands (A10) + chromagram (A12), fused",
             "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_batch": ms,
             "roofline": {"bound": "hbm", "kernel": "spectra_rf_kernel<4096>", "achieved": gbs, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
-                         "bytes_per_frame": bpf}}
+                         "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": src,
+                         "bytes_per_frame": bpf, "algorithmic_bytes_per_launch": n * bpf}}
 
 
 def drums_line(dev, reps=20, n=4096, bins=1025):
@@ -149,7 +301,7 @@ def drums_line(dev, reps=20, n=4096, bins=1025):
     return {"workload": f"drum features: {n} consecutive frames x {bins} bins of one stream (kick 3 + snare 4 band "
                         "flux, adaptive thresholds, spectral centroid)",
             "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_call": ms,
-            "roofline": {"bound": "hbm", "kernel": "drum_flux_kernel + drum_thr_kernel", "achieved": gbs,
+            "roofline": {"bound": "latency", "kernel": "drum_flux_kernel + drum_thr_kernel", "achieved": gbs,
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
                          "bytes_per_frame": bpf}}
 
@@ -177,7 +329,7 @@ def post_line(dev, reps=20, n=4096, bins=512):
     return {"workload": f"app post-processing: {n} consecutive combined spectra x {bins} bins of one stream "
                         f"({pp.n_bands} bands)",
             "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_call": ms,
-            "roofline": {"bound": "hbm", "kernel": "post_frame_kernel + post_ema_kernel", "achieved": gbs,
+            "roofline": {"bound": "latency", "kernel": "post_frame_kernel + post_ema_kernel", "achieved": gbs,
                          "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
                          "bytes_per_frame": bpf}}
 
@@ -201,16 +353,37 @@ def band_table_512(fs=FS, num_bands=512, fft_size=8192):
     return pipeline_band_table(fs, num_bands, fft_size)
 
 
-def kernel_traffic():
-    """HBM bytes per batch_kernel launch from the newest committed counter passes
-    (profiles/rNN_batch_traffic.json, written by tools/profile_round.sh + tools/summarize_round.py),
+def kernel_traffic(kind="batch"):
+    """HBM bytes per launch of the dominant kernel from the newest committed counter passes
+    (profiles/rNN_<kind>_traffic.json, written by tools/profile_round.sh + tools/summarize_round.py),
     or None."""
     import glob
-    fs = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_batch_traffic.json")))
+    fs = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{kind}_traffic.json")))
     if not fs:
         return None, None
     d = json.load(open(fs[-1]))
     return d["traffic_bytes"], os.path.relpath(fs[-1], REPO)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_calibration():
+    """The restatement-vs-reference time ratio measured in the build container
+    (tools/cpu_calibrate.py -> profiles/cpu_calibration.json), so the GPU host's port number is
+    traceable to the reference's own CPU cost."""
+    p = os.path.join(REPO, "profiles", "cpu_calibration.json")
+    if not os.path.exists(p):
+        return None
+    return json.load(open(p))
 
 
 def cpu_baseline(seconds):
@@ -231,9 +404,10 @@ def cpu_baseline(seconds):
         if time.perf_counter() - t0 > seconds and n >= 8:
             break
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "channel-frames/s", "cores": 1, "kind": "port",
+    return {"value": n / dt, "unit": "channel-frames/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{n} channel-frames of cfg2 (oracle: MRFFT 16k/8k/4k/1k + combine(512) + K-LUFS + "
-                      f"4x TP + meter deques), {dt:.1f} s, OMP_NUM_THREADS=1"}
+                      f"4x TP + meter deques), {dt:.1f} s, OMP_NUM_THREADS=1",
+            "calibration": cpu_calibration()}
 
 
 def _cpu_worker(args):
@@ -263,123 +437,101 @@ def cpu_baseline_all_cores(seconds, procs):
         res = pool.map(_cpu_worker, [(seconds, i % 2, 2 * (i // 2)) for i in range(procs)])
     n = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
-    return {"value": n / wall, "unit": "channel-frames/s", "cores": procs, "kind": "port",
+    return {"value": n / wall, "unit": "channel-frames/s", "cores": procs, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{n} channel-frames of cfg2 over {procs} processes (one stream each, oracle loop with "
                       f"meter state), {wall:.1f} s, OMP_NUM_THREADS=1"}
 
 
-def main():
-    a = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started here before any GPU call (no exec from a GPU process)
+        sys.exit(launch_ranks(a.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}")
+    standin = a.standin is not None
     cpu_all = None
-    if world == 1 and not a.no_cpu_baseline and a.cpu_procs > 1:
+    if world == 1 and not a.no_cpu_baseline and a.cpu_procs > 1 and not standin:
         # before any GPU call: the workers are forked from this process
         cpu_all = cpu_baseline_all_cores(a.cpu_seconds, a.cpu_procs)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    be = importlib.import_module(a.standin).Backend(local) if standin else DeviceBackend(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-    from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
-
-    # per-rank shard of the cfg2 workload: seeds (2r, 2r+1) per shard
-    x = torch.from_numpy(cfg2_input(FRAMES, W, seed_l=2 * rank, seed_r=2 * rank + 1)).to(dev)
-    eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=T, n_channels=C, device=local)
-    ncf = FRAMES * C
-    bufs = []
-    for _ in range(2):
-        bufs.append({"combined": torch.empty(ncf, T, device=dev), "lufs_inst": torch.empty(ncf, device=dev),
-                     "true_peak_db": torch.empty(ncf, device=dev),
-                     "meters": torch.empty(ncf, 5, dtype=torch.float64, device=dev)})
+        if standin:
+            dist.init_process_group(be.dist_backend)
+        else:
+            dist.init_process_group(be.dist_backend, device_id=be.dev)
     gather = world > 1 and not a.no_gather
-    if gather:
-        from omega_gpu import dist as D
-        # per-frame output vector: combined[512] + lufs + tp + 5 meters (as float32) = 519 floats
-        packs = [torch.empty(ncf, D.pack_width(T), device=dev) for _ in range(2)]
-        recv = [[torch.empty(ncf, D.pack_width(T), device=dev) for _ in range(world)] if rank == 0 else None
-                for _ in range(2)]
-        pending = [None, None]
 
-    def step(i):
-        b = i % 2
-        if gather and pending[b] is not None:
-            pending[b].wait()
-        o = eng.process_frames(x, FRAMES, C * W, W, meters=True, out=bufs[b])
-        if gather:
-            pending[b] = D.gather_to_root(D.pack_outputs(o, T, packs[b]), recv[b], async_op=True)
+    frames = a.frames
+    dt, got, lay = measure(be, rank, world, frames, a.steps, a.warmup, gather)
+    ncf = frames * C
+    value = ncf * world * a.steps / dt
+    if a.dump and rank == 0 and got is not None:
+        np.save(a.dump, torch.stack([g.cpu() for g in got]).numpy())
 
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for i in range(a.warmup):
-        step(i)
-    if gather:
-        for p in pending:
-            if p is not None:
-                p.wait()
-        pending = [None, None]
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(i)
-    if gather:
-        for p in pending:
-            if p is not None:
-                p.wait()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    dt = t1 - t0
-    if world > 1:
-        import torch.distributed as dist
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    total_cf = ncf * world * a.steps
-    value = total_cf / dt
-
-    kt_ms, kcf = kernel_time_ms(eng, x)
-    flop_launch = (FLOP_FFT + FLOP_KW + FLOP_TP) * kcf
-    achieved = flop_launch / (kt_ms * 1e-3) / 1e12
-    traffic, traffic_src = kernel_traffic()
+    roof = None
+    cfg4 = None
+    if not standin:
+        kt_ms, kcf = kernel_time_ms(be.eng, be.input(frames, 2 * rank, 2 * rank + 1))
+        flop_launch = (FLOP_FFT + FLOP_KW + FLOP_TP) * kcf
+        achieved = flop_launch / (kt_ms * 1e-3) / 1e12
+        traffic, traffic_src = kernel_traffic("batch")
+        roof = {"bound": "valu", "kernel": "batch_kernel (K-weighting + LUFS, 16k/8k/4k/1k FFT + combine, "
+                                           "4x true peak; fp32)",
+                "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
+                "kernel_ms": kt_ms, "flop_per_launch": flop_launch,
+                "traffic_unit": "bytes per launch (HBM, FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": kcf * BYTES_CF,
+                "note": "fp32 VALU-bound (no MFMA: nothing here is a dense contraction); algorithmic flops per "
+                        "channel-frame = SURVEY.md §8(d) FFT 1.09 M + KW 0.67 M + TP 3.33 M (the reference's "
+                        "resample algorithm); kernel_ms = HIP-event average of 20 back-to-back launches on the "
+                        "launch stream"}
+        if not a.no_cfg4:
+            dt4, _, _ = measure(be, rank, world, FRAMES_CFG4, a.cfg4_steps, 3, gather)
+            ncf4 = FRAMES_CFG4 * C
+            cfg4 = {"workload": f"cfg4 per-GPU shard: {FRAMES_CFG4} stereo frames x 16384 per GPU "
+                                f"({FRAMES_CFG4 * world} stereo frames over {world} GPU(s); BASELINE cfg4 = 32768 "
+                                "over 8), same per-step path as the headline line" +
+                                (", packed outputs gathered to rank 0 over RCCL each step" if gather else ""),
+                    "value": ncf4 * world * a.cfg4_steps / dt4, "unit": "channel-frames/s",
+                    "ms_per_step": dt4 / a.cfg4_steps * 1e3, "steps": a.cfg4_steps,
+                    "channel_frames_per_gpu": ncf4, "global_stereo_frames": FRAMES_CFG4 * world}
     if rank == 0:
         cpu = None
-        if world == 1 and not a.no_cpu_baseline:
+        if world == 1 and not a.no_cpu_baseline and not standin:
             cpu = cpu_baseline(a.cpu_seconds)
         line = {
-            "metric": "audio frames/sec (multi-res FFT + LUFS + TruePeak) at 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": value, "unit": "channel-frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic cfg2 frames (0.25 sine 440/997 Hz + 0.05 N(0,1), seeds per rank)",
-            "config": {"workload": "cfg2: 256 stereo frames x 16384 samples per GPU; MRFFT 16k/8k/4k/1k + "
+            "config": {"workload": f"cfg2: {frames} stereo frames x 16384 samples per GPU; MRFFT 16k/8k/4k/1k + "
                                    "combine(512) + K-weighted LUFS + 4x true peak + meter aggregates",
                        "channel_frames_per_gpu": ncf, "frame_samples": W, "target_bins": T,
-                       "parallelism": f"frames sharded over {world} GPU(s)" + (", RCCL gather to rank 0" if gather else "")},
-            "roofline": {"bound": "mfma", "kernel": "batch_kernel (K-weighting + LUFS, 16k/8k/4k/1k FFT + combine, "
-                                                    "4x true peak; fp32)",
-                         "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "kernel_ms": kt_ms, "flop_per_launch": flop_launch,
-                         "traffic_unit": "bytes per launch (HBM, FETCH_SIZE x2 + WRITE_SIZE)",
-                         "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": kcf * (4 * W + 4 * (T + 2)),
-                         "note": "fp32 VALU/LDS-bound (no MFMA: the fp32 MFMA peak equals the fp32 vector peak, "
-                                 "quoted as the roof); algorithmic flops per channel-frame = SURVEY.md §8(d) "
-                                 "FFT 1.09 M + KW 0.67 M + TP 3.33 M (the reference's resample algorithm); "
-                                 "kernel_ms = HIP-event average of 20 back-to-back launches on the launch stream"},
+                       "parallelism": f"frames sharded over {world} GPU(s)" +
+                                      (", packed outputs gathered to rank 0 over RCCL each step" if gather else "")},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
         }
-        if world == 1 and not a.no_cfg3:
-            line["cfg3"] = cfg3_line(dev)
-            line["drums"] = drums_line(dev)
-            line["app_post"] = post_line(dev)
+        if standin:
+            line["backend"] = f"stand-in {a.standin} (CPU, {be.dist_backend}); not a measurement"
+        if cfg4 is not None:
+            line["cfg4"] = cfg4
+        if world == 1 and not a.no_cfg3 and not standin:
+            line["cfg3"] = cfg3_line(be.dev)
+            line["drums"] = drums_line(be.dev)
+            line["app_post"] = post_line(be.dev)
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -58,11 +58,13 @@ def _worker(rank, world, port, x, q):
         # whole streams per rank: shard the frame axis, every rank keeps all channels of its frames
         fa, fb = D.shard_range(F, rank, world)
         out = _shard_outputs(x, fa * C, fb * C)
-        p = D.pack_outputs(out, T)
+        lay = D.PackedLayout((fb - fa) * C, T)
+        p = lay.pack(out)
         recv = [torch.empty_like(p) for _ in range(world)] if rank == 0 else None
         D.gather_to_root(p, recv, async_op=True).wait()
         if rank == 0:
-            q.put(torch.cat(recv).numpy())
+            g = D.unpack_gathered(recv, lay)
+            q.put({k: v.numpy() for k, v in g.items()})
     finally:
         dist.destroy_process_group()
 
@@ -82,10 +84,10 @@ def test_pack_roundtrip():
     n = 3
     out = {"combined": torch.rand(n, T), "lufs_inst": torch.rand(n), "true_peak_db": torch.rand(n),
            "meters": torch.rand(n, 5, dtype=torch.float64)}
-    u = D.unpack_outputs(D.pack_outputs(out, T), T)
-    for k in ("combined", "lufs_inst", "true_peak_db"):
+    lay = D.PackedLayout(n, T)
+    u = lay.views(lay.pack(out))
+    for k in out:
         assert torch.equal(u[k], out[k])
-    assert torch.allclose(u["meters"], out["meters"].float())
 
 
 def test_gloo_world2_gather_matches_single_process():
@@ -104,7 +106,7 @@ def test_gloo_world2_gather_matches_single_process():
         p.join(timeout=60)
         assert p.exitcode == 0
     # single process, same sharding of streams (meter state restarts per shard, as per rank)
-    ref = np.concatenate([D.pack_outputs(_shard_outputs(x, a * 2, b * 2), T).numpy()
-                          for a, b in (D.shard_range(4, r, world) for r in range(world))])
-    np.testing.assert_array_equal(got, ref)
-    assert got.shape == (8, T + 7)
+    shards = [_shard_outputs(x, a * 2, b * 2) for a, b in (D.shard_range(4, r, world) for r in range(world))]
+    for k in got:
+        np.testing.assert_array_equal(got[k], np.concatenate([s[k].numpy() for s in shards]), err_msg=k)
+    assert got["combined"].shape == (8, T) and got["meters"].shape == (8, 5)

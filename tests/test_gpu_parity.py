@@ -327,6 +327,46 @@ def test_cfg2_meter_state_matches_oracle_sequence(cfg2):
         np.testing.assert_allclose(out["meters"].reshape(256, 2, 5)[:, c], ref, rtol=0, atol=1e-9)
 
 
+def test_cfg4_shard_packed_outputs_match_oracle():
+    """BASELINE cfg4's per-GPU shard (4096 stereo frames x 16384 = 8192 channel-frames, two meter
+    chunks per channel) through bench.py's own zero-copy packed output block: sampled frames against
+    the oracle (first/last, both sides of the meter-chunk boundary), the meter aggregates of all 4096
+    frames per channel against the oracle's sequential calculate_lufs calls on the device's
+    instantaneous values, and full-size properties (finite, TP >= sample peak, bitwise repeatable)."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    from omega_gpu import dist as D
+    F = 4096
+    x = S.cfg2_batch(F, seed_l=6, seed_r=7)  # rank 3's seeds
+    xd = torch.from_numpy(x).cuda()
+    eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+    lay = D.PackedLayout(2 * F, 512)
+    bufs = [lay.alloc("cuda"), lay.alloc("cuda")]
+    eng.process_frames(xd, F, 2 * 16384, 16384, meters=True, out=lay.views(bufs[0]))
+    torch.cuda.synchronize()
+    out = {k: v.cpu().numpy() for k, v in lay.views(bufs[0]).items()}
+    for f, c in ((0, 0), (1, 1), (2047, 0), (2048, 1), (3001, 0), (4095, 1)):
+        _, comb, li, tp = R.full_frame(x[f, c])
+        cf = f * 2 + c
+        assert normwise(out["combined"][cf], comb) < SPEC_TOL, (f, c)
+        assert abs(out["lufs_inst"][cf] - li) < LU_TOL, (f, c)
+        assert abs(out["true_peak_db"][cf] - tp) < TP_TOL_DB, (f, c)
+    assert np.isfinite(out["combined"]).all() and np.isfinite(out["meters"]).all()
+    peak_db = 20 * np.log10(np.abs(x).max(axis=2)).reshape(-1)
+    assert (out["true_peak_db"] >= peak_db - 1e-4).all()
+    li = out["lufs_inst"].reshape(F, 2)
+    tp = out["true_peak_db"].reshape(F, 2)
+    for c in (0, 1):
+        st = R.MeterState(FS)
+        ref = np.array([list(st.update(np.ones(1), float(li[f, c]), float(tp[f, c])).values()) for f in range(F)])
+        np.testing.assert_allclose(out["meters"].reshape(F, 2, 5)[:, c], ref, rtol=0, atol=1e-9)
+    # the same batch again into the other buffer (a fresh meter stream): bitwise identical
+    eng.reset_meters()
+    eng.process_frames(xd, F, 2 * 16384, 16384, meters=True, out=lay.views(bufs[1]))
+    torch.cuda.synchronize()
+    assert torch.equal(bufs[0], bufs[1])
+
+
 def test_stream_layout_hop(cfg2):
     """Stream layout: overlapping frames of one planar stream via frame_stride = hop."""
     import torch
