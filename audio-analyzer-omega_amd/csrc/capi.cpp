@@ -180,6 +180,11 @@ struct omega_ctx {
   unsigned* d_kw_done = nullptr;  // batch_kernel's K-weighting workgroups count themselves in here
   unsigned kw_issued = 0;         // K-weighting workgroups launched with the count on (wraps)
   unsigned q_issued = 0;          // LUFS-meter query workgroups launched with the count on (d_kw_done[1])
+  // device-side poll expiry flags (host-mapped: [0] meter prep, [1] join), checked by
+  // check_device_err; the poll bound (OMEGA_POLL_LIMIT, a test knob)
+  unsigned* h_err = nullptr;
+  unsigned* d_err = nullptr;
+  int poll_limit = 1 << 22;
   int batch_order = 3;            // role order of the batch launch (enqueue_batch; OMEGA_BATCH_ORDER)
   bool res_independent = false;  // no combine target has several owners: resolution kernels commute
   hipEvent_t ev_kw = nullptr;
@@ -588,6 +593,12 @@ int build_meter_state(omega_ctx* c) {
   if (!e) e = dalloc(c, &c->d_gsum, (size_t)C * (kMeterSeqCap + 1));
   if (!e) e = dalloc(c, &c->d_kw_done, 4);
   if (e) return e;
+  if (!c->h_err) {
+    HIPC(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_err), 2 * sizeof(unsigned),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    c->h_err[0] = c->h_err[1] = 0;
+    HIPC(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_err), c->h_err, 0));
+  }
   HIPC(c, hipMemset(c->d_kw_done, 0, 4 * sizeof(unsigned)));
   c->kw_issued = c->q_issued = 0;
   return omega_meter_reset(c);
@@ -687,6 +698,8 @@ std::vector<MeterPrepParams> meter_chunks(omega_ctx* c, const float* lufs, const
     p.short_len = c->cfg.short_len;
     p.int_len = c->cfg.integrated_len;
     p.peak_len = c->cfg.peak_len;
+    p.poll_limit = c->poll_limit;
+    p.err_word = c->d_err;
     p.gate = (float)c->cfg.gate_lufs;
     p.core = c->d_core;
     p.ext = c->d_ext;
@@ -967,6 +980,7 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   if (const char* rs = std::getenv("OMEGA_RF_SIZES")) c->rf_sizes = std::atoi(rs) & ((1 << 14) | (1 << 13));
   if (const char* gr = std::getenv("OMEGA_GRAPHS")) c->use_graph = std::atoi(gr) != 0;
   if (const char* bo = std::getenv("OMEGA_BATCH_ORDER")) c->batch_order = std::atoi(bo);
+  if (const char* pl = std::getenv("OMEGA_POLL_LIMIT")) c->poll_limit = std::atoi(pl) > 0 ? std::atoi(pl) : 1;
   if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
     const int v = std::atoi(lay);
     c->layout = v < 0 || v > 3 ? 3 : v;
@@ -1176,6 +1190,21 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   return 0;
 }
 
+// A device-side ordering wait that expired (meters.hip: the prep kernel's wait for the batch's
+// K-weighting count, the join of the LUFS meters into the caller's stream) means some meter aggregates
+// were computed from, or returned before, incomplete inputs: report it once as OMEGA_EHIP.
+int check_device_err(omega_ctx* c) {
+  if (!c->h_err) return 0;
+  volatile unsigned* e = c->h_err;
+  const unsigned prep = e[0], join = e[1];
+  if (!prep && !join) return 0;
+  e[0] = 0;
+  e[1] = 0;
+  return fail(c, OMEGA_EHIP, "device-side meter ordering wait expired (%s%s%s): meter aggregates of an earlier call "
+              "may be stale", prep ? "meter prep waiting for the K-weighting count" : "", prep && join ? ", " : "",
+              join ? "caller's stream joining the LUFS meters" : "");
+}
+
 void omega_destroy(omega_ctx* c) {
   if (!c) return;
   if (c->device >= 0) (void)hipSetDevice(c->device);
@@ -1189,6 +1218,7 @@ void omega_destroy(omega_ctx* c) {
     if (b.p) (void)hipFree(b.p);
   drop_graphs(c);
   if (c->d_tpx) (void)hipFree(c->d_tpx);
+  if (c->h_err) (void)hipHostFree(c->h_err);
   for (hipStream_t st : {c->cap, c->fork[0], c->fork[1]})
     if (st) (void)hipStreamDestroy(st);
   for (hipEvent_t ev : {c->ev_fork, c->ev_join[0], c->ev_join[1], c->ev_kw})
@@ -1219,7 +1249,7 @@ int omega_set_graphs(omega_ctx* c, int enable) {
 int omega_synchronize(omega_ctx* c) {
   if (!c) return OMEGA_EINVAL;
   HIPC(c, hipStreamSynchronize(c->stream));
-  return 0;
+  return check_device_err(c);
 }
 
 int omega_meter_reset(omega_ctx* c) {
@@ -1239,6 +1269,7 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
                          const omega_outputs* out, int mem) {
   if (!c || !out) return OMEGA_EINVAL;
   if (!x || n_frames < 0) return fail(c, OMEGA_EINVAL, "null input or negative frame count");
+  if (int e = check_device_err(c)) return e;
   if (n_frames == 0) return 0;
   const int C = c->cfg.n_channels, W = c->cfg.frame_size, T = c->cfg.target_bins;
   const int64_t ncf = n_frames * C;
@@ -1464,6 +1495,7 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
                        int mem) {
   if (!c || !lufs_inst || !tp_db || !meters) return OMEGA_EINVAL;
   if (n_frames <= 0) return n_frames == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  if (int e = check_device_err(c)) return e;
   HIPC(c, hipSetDevice(c->device));
   const int64_t ncf = n_frames * c->cfg.n_channels;
   std::vector<HostOut> outs;

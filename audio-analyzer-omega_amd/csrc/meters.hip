@@ -160,10 +160,16 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     // the batch's LUFS_inst values come from batch_kernel on another stream: one lane polls the count
     // (relaxed, bounded), then ONE agent-scope acquire before any wave reads them
     if (tid == 0) {
-      for (int i = 0; i < (1 << 22); ++i) {
-        if ((int)(__hip_atomic_load(p.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - p.wait_target) >= 0) break;
+      bool met = false;
+      for (int i = 0; i < p.poll_limit; ++i) {
+        if ((int)(__hip_atomic_load(p.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - p.wait_target) >= 0) {
+          met = true;
+          break;
+        }
         __builtin_amdgcn_s_sleep(4);
       }
+      if (!met && p.err_word)
+        __hip_atomic_store(p.err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -534,10 +540,16 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
   }
   if (p.join_ctr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     // the join: this stream's work completes only after the side stream's query workgroups (bounded)
-    for (int i = 0; i < (1 << 22); ++i) {
-      if ((int)(__hip_atomic_load(p.join_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - p.join_target) >= 0) break;
+    bool met = false;
+    for (int i = 0; i < p.poll_limit; ++i) {
+      if ((int)(__hip_atomic_load(p.join_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - p.join_target) >= 0) {
+        met = true;
+        break;
+      }
       __builtin_amdgcn_s_sleep(4);
     }
+    if (!met && p.err_word)
+      __hip_atomic_store(p.err_word + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
 }

@@ -142,6 +142,11 @@ struct MeterPrepParams {
   unsigned* q_done;
   unsigned* join_ctr;
   unsigned join_target;
+  // bounded polls: at most poll_limit iterations; on expiry the kernel stores 1 into err_word[0] (prep)
+  // or err_word[1] (join) -- host-mapped memory the host checks in omega_synchronize and the next call
+  // (OMEGA_EHIP instead of silently stale meters)
+  int poll_limit;
+  unsigned* err_word;
 };
 
 struct BandParams {

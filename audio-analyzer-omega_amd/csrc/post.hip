@@ -8,11 +8,18 @@
 //                                 :1011-1036 band means, sqrt, clamp to [0, 1]
 //                                 :1041-1056 frequency-dependent band EMA across frames
 // in float32 as numpy runs them (in-place multiplies by weak Python scalars; the percentile's virtual
-// index and gamma in float32).
+// index and gamma in float32; np.mean as numpy's float32 pairwise sum, divided in float64 by the
+// np.intp count and rounded to float32).
+//
+// Bit-exactness needs every float32 operation rounded on its own: floating-point contraction is off
+// for this file (HIP's default -ffp-contract=fast fused the percentile's lerp into an FMA, 1 ulp off
+// the reference's reference value on some frames -- then every bin of such a frame).
 //   post_frame_kernel: one 256-thread workgroup per frame (independent frames).
 //   post_ema_kernel: one workgroup, one thread per band, the frames in order (the EMA recurrence).
 #include "fft.hpp"
 #include "params.hpp"
+
+#pragma clang fp contract(off)
 
 namespace omega {
 
@@ -33,11 +40,52 @@ __device__ __forceinline__ T block_reduce(T v, T* red, int t, Op op) {
   return r;
 }
 
+// numpy's pairwise_sum for contiguous float32 (numpy/_core/src/umath/loops_utils.h.src): below 8
+// elements a plain running sum, up to 128 eight interleaved accumulators combined as
+// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) plus the tail, above that the two halves split at a
+// multiple of 8 below n / 2. np.add.reduce starts from the identity 0 (0 + s == s).
+__device__ __noinline__ float np_pairwise_leaf(const float* a, int n) {
+  if (n < 8) {
+    float r = 0.f;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  }
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+template <int D>
+__device__ float np_pairwise_sum(const float* a, int n) {
+  if constexpr (D == 0) {
+    return np_pairwise_leaf(a, n);
+  } else {
+    if (n <= 128) return np_pairwise_leaf(a, n);
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return np_pairwise_sum<D - 1>(a, n2) + np_pairwise_sum<D - 1>(a + n2, n - n2);
+  }
+}
+
+// np.mean of a float32 range: float32(float64(pairwise sum) / float64(n)) (_methods._mean divides the
+// float32 sum by an np.intp count, which promotes to float64)
+__device__ __forceinline__ float np_mean_f32(const float* a, int n) {
+  static_assert(kPostMaxBins <= 128 << 5, "pairwise recursion depth");
+  return (float)((double)np_pairwise_sum<5>(a, n) / (double)n);
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) {
   __shared__ float s[kPostMaxBins];
-  __shared__ double redd[kPostThreads / 64];
   __shared__ float redf[kPostThreads / 64];
   __shared__ float pv[2];
   const int t = threadIdx.x, T = p.T;
@@ -53,30 +101,36 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
     s[i] = v;
   }
   __syncthreads();
-  // 2) content type from the range means (omega4_main.py:805-840; voice detection is not on the path)
-  auto dsum = [](double a, double b) { return a + b; };
-  auto fmx = [](float a, float b) { return fmaxf(a, b); };
-  double sb = 0.0, sv = 0.0, sh = 0.0, st = 0.0;
-  float mx = -INFINITY;
-  for (int i = t; i < T; i += kPostThreads) {
-    const double v = s[i];
-    if (i < p.be) sb += v;
-    if (i >= p.vs && i < p.ve) sv += v;
-    if (i >= p.hs) sh += v;
-    st += v;
-    mx = fmaxf(mx, s[i]);
+  // 2) content type from the range means (omega4_main.py:805-840; voice detection is not on the path):
+  // four np.mean calls, one thread each (waves 0-3); the max and a NaN flag by block reduction
+  __shared__ float means[4];
+  __shared__ int anynan;
+  if (t == 0) anynan = 0;
+  {
+    const int w = t >> 6;
+    if ((t & 63) == 0) {
+      float m = 0.f;
+      if (w == 0 && p.be < T) m = np_mean_f32(s, p.be);
+      if (w == 1 && p.ve < T) m = np_mean_f32(s + p.vs, p.ve - p.vs);
+      if (w == 2 && p.hs < T) m = np_mean_f32(s + p.hs, T - p.hs);
+      if (w == 3) m = np_mean_f32(s, T);
+      means[w] = m;
+    }
   }
-  sb = block_reduce(sb, redd, t, dsum);
-  sv = block_reduce(sv, redd, t, dsum);
-  sh = block_reduce(sh, redd, t, dsum);
-  st = block_reduce(st, redd, t, dsum);
-  mx = block_reduce(mx, redf, t, fmx);
-  const float eb = p.be < T ? (float)(sb / p.be) : 0.f;
-  const float ev = p.ve < T ? (float)(sv / (p.ve - p.vs)) : 0.f;
-  const float eh = p.hs < T ? (float)(sh / (T - p.hs)) : 0.f;
-  const float et = (float)(st / T);
+  auto fmx = [](float a, float b) { return fmaxf(a, b); };
+  float mx = -INFINITY;
+  bool nan_here = false;
+  for (int i = t; i < T; i += kPostThreads) {
+    mx = fmaxf(mx, s[i]);
+    nan_here |= isnan(s[i]);
+  }
+  __syncthreads();  // anynan initialised
+  if (nan_here) anynan = 1;
+  mx = block_reduce(mx, redf, t, fmx);  // (its barriers publish means[] and anynan)
+  const bool has_nan = anynan != 0;
+  const float eb = means[0], ev = means[1], eh = means[2], et = means[3];
   int content = 0;  // 0 instrumental, 1 vocal, 2 bass-heavy
-  if (et > 0.f) {
+  if (et > 0.f) {  // (NaN means fail every comparison, as in numpy)
     const float br = eb / et, vr = ev / et;
     if (br > 0.6f)
       content = 2;
@@ -84,7 +138,10 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
       content = 1;
   }
   // 3) 98th percentile (numpy 'linear', float32): the values of sorted ranks p_lo and p_hi
-  if (mx > 0.f) {
+  // np.max and np.percentile propagate NaN: `nan > 0` is false, no normalisation
+  if (mx > 0.f && !has_nan) {
+    if (t == 0) pv[0] = pv[1] = NAN;
+    __syncthreads();
     for (int i = t; i < T; i += kPostThreads) {
       const float v = s[i];
       int r = 0;
@@ -111,7 +168,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
     float m = -INFINITY;
     for (int i = t; i < T; i += kPostThreads) m = fmaxf(m, s[i]);
     m = block_reduce(m, redf, t, fmx);
-    if (m > 0.f)
+    if (m > 0.f && !has_nan)
       for (int i = t; i < T; i += kPostThreads) s[i] = __fdiv_rn(s[i], m);
     __syncthreads();
   }
@@ -121,9 +178,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
     const int lo = p.bs[b], hi = p.bend[b];
     float v;
     if (hi > lo) {
-      double a = 0.0;
-      for (int i = lo; i < hi; ++i) a += s[i];
-      v = (float)(a / (hi - lo));
+      v = np_mean_f32(s + lo, hi - lo);
     } else {
       v = s[lo];
     }

@@ -105,7 +105,8 @@ class SpectrumPostProcessor:
         """spectra: [F, T] float32, host numpy or device torch (results come back the same way)."""
         import torch
         host = not _is_torch(spectra)
-        x = torch.as_tensor(np.ascontiguousarray(np.atleast_2d(spectra), np.float32)).cuda() if host else spectra
+        dev = torch.device("cuda", self._eng.device)
+        x = torch.as_tensor(np.ascontiguousarray(np.atleast_2d(spectra), np.float32)).to(dev) if host else spectra
         if x.dtype != torch.float32 or x.dim() != 2 or x.shape[1] != self.n_bins or x.stride(1) != 1:
             raise ValueError(f"spectra must be [F, {self.n_bins}] float32 rows")
         F = x.shape[0]

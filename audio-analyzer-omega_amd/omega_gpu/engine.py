@@ -104,7 +104,11 @@ class Engine:
         self._check(L.lib().omega_synchronize(self._ctx))
 
     def _bind_stream(self, tensor):
+        """Enqueue on torch's current stream of the tensor's device, which must be this context's GPU
+        (a pointer on another device would be read by this device's kernels)."""
         import torch
+        if not tensor.is_cuda or tensor.device.index != self.device:
+            raise ValueError(f"device tensor on {tensor.device}, but this engine runs on cuda:{self.device}")
         self._check(L.lib().omega_set_stream(self._ctx, C.c_void_p(torch.cuda.current_stream(tensor.device).cuda_stream)))
 
     def reset_meters(self):
