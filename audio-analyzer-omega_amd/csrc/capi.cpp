@@ -606,6 +606,7 @@ int build_meter_state(omega_ctx* c) {
 
 SpectralParams spectral_params(omega_ctx* c) {
   SpectralParams p{};
+  p.tp_phases = 0xE;
   p.C = c->cfg.n_channels;
   p.n_res = c->cfg.n_res;
   p.rf_sizes = c->rf_sizes;
@@ -1425,7 +1426,14 @@ int omega_combine(omega_ctx* c, const float* const* mags, int64_t n_cf, float* o
 }
 
 int omega_true_peak(omega_ctx* c, const float* x, int64_t n, int32_t m, float* out_db, int mem) {
+  return omega_true_peak_os(c, x, n, m, 4, out_db, mem);
+}
+
+int omega_true_peak_os(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t oversampling, float* out_db,
+                       int mem) {
   if (!c || !x || !out_db) return OMEGA_EINVAL;
+  if (oversampling != 1 && oversampling != 2 && oversampling != 4)
+    return fail(c, OMEGA_EUNSUP, "true peak: oversampling %d unsupported (1, 2, 4)", oversampling);
   if (!is_pow2_in(m, 512, 16384)) return fail(c, OMEGA_EUNSUP, "true peak: frame length %d unsupported", m);
   if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
   HIPC(c, hipSetDevice(c->device));
@@ -1453,6 +1461,7 @@ int omega_true_peak(omega_ctx* c, const float* x, int64_t n, int32_t m, float* o
   if (!e) e = tp_scratch(c, m, n, &sp.tp_scratch);
   if (e) return e;
   sp.rot = rot;
+  sp.tp_phases = oversampling == 4 ? 0xE : (oversampling == 2 ? 0x4 : 0);
   HIPC(c, tp_launch(c, m, sp, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;

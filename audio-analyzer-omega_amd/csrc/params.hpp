@@ -43,6 +43,9 @@ struct SpectralParams {
   float* tp_out;      // [n_cf] or nullptr
   const float2* rot;  // [W/2 + 1] exp(+2 pi i k / (4W))
   float4* tp_scratch;  // [n_cf, W/4] half-spectrum pairs of the 512-thread true-peak kernel (L2-resident)
+  // true-peak phases y(n + P/4) computed besides the samples (P = 0): bit P set. 0xE = 4x
+  // oversampling (the reference's default), 0x4 = 2x (n + 1/2 only), 0 = 1x (the samples)
+  int tp_phases;
   const float2* tw[kMaxLog2];  // tw[l][m] = exp(-2 pi i m / 2^l)
   int rf_sizes;  // host-side launch choice: bit log2(N) set = resolution size N runs on the register-FFT kernel
 };

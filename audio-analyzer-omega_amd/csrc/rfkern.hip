@@ -93,6 +93,7 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
       const float2 rk = cmul(rhol, make_float2(kCos128[r], kSin128[r]));
       y[r] = cmul(y[r], rk);
     });
+    if (!((p.tp_phases >> P) & 1)) continue;  // phase not requested (oversampling 2 or 1)
     __syncthreads();  // the previous transform's last exchange reads are done
     {
       float2* bo = buf + FFT::s3(tl);

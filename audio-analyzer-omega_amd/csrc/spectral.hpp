@@ -182,6 +182,18 @@ __device__ __forceinline__ void truepeak_body(const SpectralParams& p, int64_t c
     asm volatile("" : "+v"(tl));
     float2* zin = zsel ? bufB : bufA;
     float2* zalt = zsel ? bufA : bufB;
+    if (!((p.tp_phases >> P) & 1)) {  // phase not requested (oversampling 2 or 1): advance the rotations only
+      static_for<0, PB>([&](auto b) {
+        const int k = tl + b * NTH;
+        if (NP % NTH == 0 || k < NP) {
+          const float2 r1 = rk[b];
+          Xlo[b] = cmul(Xlo[b], r1);
+          Xhi[b] = cmul(Xhi[b], make_float2(kS2 * (r1.x + r1.y), kS2 * (r1.x - r1.y)));
+          if (k == 0) Xmid = cmul(Xmid, rh);
+        }
+      });
+      continue;
+    }
     static_for<0, PB>([&](auto b) {
       const int k = tl + b * NTH;
       if (NP % NTH == 0 || k < NP) {
@@ -265,6 +277,10 @@ __device__ __forceinline__ void truepeak_l2_body(const SpectralParams& p, int64_
     twl.launder();
     asm volatile("" : "+v"(tl));
     __syncthreads();  // the previous transform's last pass has read buf
+    if (!((p.tp_phases >> P) & 1)) {  // phase not requested: only the running Nyquist-mirror rotation
+      if (tl == 0) Xmid = cmul(Xmid, rh);
+      continue;
+    }
     static_for<0, PB>([&](auto b) {
       const int k = tl + b * NTH;
       const float4 xp = xs[b * NTH + tl];

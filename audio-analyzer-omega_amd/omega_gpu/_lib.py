@@ -67,6 +67,7 @@ EXPORTS = {
                                 C.c_void_p, C.c_void_p, C.c_int]),
     "omega_combine": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int64, C.c_void_p, C.c_int]),
     "omega_true_peak": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int]),
+    "omega_true_peak_os": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_int]),
     "omega_k_weighting": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p,
                                     C.c_int]),
     "omega_weighting": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p,

@@ -184,11 +184,11 @@ class Engine:
         self._check(L.lib().omega_combine(self._ctx, ptrs, int(n_cf), out.ctypes.data, L.MEM_HOST))
         return out
 
-    def true_peak(self, x: np.ndarray) -> np.ndarray:
+    def true_peak(self, x: np.ndarray, oversampling: int = 4) -> np.ndarray:
         x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float32)
         out = np.empty(x.shape[0], np.float32)
-        self._check(L.lib().omega_true_peak(self._ctx, x.ctypes.data, x.shape[0], x.shape[1], out.ctypes.data,
-                                            L.MEM_HOST))
+        self._check(L.lib().omega_true_peak_os(self._ctx, x.ctypes.data, x.shape[0], x.shape[1], int(oversampling),
+                                               out.ctypes.data, L.MEM_HOST))
         return out
 
     def weighting(self, x: np.ndarray, mode: str = "K", weighted: bool = True):

@@ -7,7 +7,10 @@ per-stream history). Filter coefficients are derived in the library (closed form
 scipy.signal.butter / lfilter_zi) and exposed here for inspection.
 
 Frames must be a power of two between 512 and 16384 samples: other lengths (the reference accepts
-any length > 9) are logged and leave the meters unchanged -- see DESIGN.md 'Scope'.
+any length > 9) are logged and leave the meters unchanged -- see DESIGN.md 'Scope'. Nothing here
+raises to the caller (the reference's convention): errors are logged and the previous values (or, for
+the weighted signal, zeros) returned. calculate_true_peak supports oversampling 1, 2 and 4 (the
+reference's default; 1 and 2 are phase subsets of the 4x polyphase transform).
 """
 from __future__ import annotations
 
@@ -56,24 +59,32 @@ class ProfessionalMetering:
 
     def apply_k_weighting(self, audio_data: np.ndarray) -> np.ndarray:
         """professional_meters.py:129-153 (returned as float64 like scipy's filtfilt)."""
-        w, _ = self._eng.weighting(self._frame(audio_data), "K")
-        return w[0].astype(np.float64)
+        try:
+            w, _ = self._eng.weighting(self._frame(audio_data), "K")
+            return w[0].astype(np.float64)
+        except Exception as e:
+            logger.error("apply_k_weighting: %s", e)
+            return np.zeros(len(audio_data), np.float64)
 
     def apply_weighting(self, audio_data: np.ndarray) -> np.ndarray:
-        """professional_meters.py:220-229: K and Z are implemented on the device."""
+        """professional_meters.py:220-229: K and Z are implemented on the device; A and C are logged
+        and give zeros (in the reference app only K is reachable: SURVEY.md §8(a) A7)."""
         if self.weighting_mode == "Z" or self.weighting_mode not in ("K", "A", "C"):
             return audio_data
         if self.weighting_mode != "K":
-            raise UnsupportedError(-4, f"weighting mode {self.weighting_mode} not implemented")
+            logger.error("apply_weighting: weighting mode %s not implemented on the device", self.weighting_mode)
+            return np.zeros(len(audio_data), np.float64)
         return self.apply_k_weighting(audio_data)
 
     def calculate_true_peak(self, audio_data: np.ndarray, oversampling: int = 4) -> float:
         """professional_meters.py:283-299 (float32 result for float32 input, like scipy)."""
         if len(audio_data) == 0:
             return -100.0
-        if oversampling != 4:
-            raise UnsupportedError(-4, "only 4x oversampling is implemented")
-        return np.float32(self._eng.true_peak(self._frame(audio_data))[0])
+        try:
+            self.current_true_peak = np.float32(self._eng.true_peak(self._frame(audio_data), oversampling)[0])
+        except Exception as e:
+            logger.error("calculate_true_peak: %s", e)
+        return self.current_true_peak
 
     def calculate_lufs(self, audio_data: np.ndarray) -> Dict[str, float]:
         """professional_meters.py:231-281."""
@@ -85,8 +96,8 @@ class ProfessionalMetering:
             _, li = self._eng.weighting(x, mode, weighted=False)
             tp = self._eng.true_peak(x)
             m = self._eng.meter_update(li, tp, 1)[0]
-        except UnsupportedError as e:
-            logger.error(f"calculate_lufs: {e}")
+        except Exception as e:
+            logger.error("calculate_lufs: %s", e)
             return self.current_lufs
         self.current_lufs["momentary"] = np.float64(m[0])
         self.current_lufs["short_term"] = np.float64(m[1])

@@ -16,6 +16,7 @@
  *                          W samples have arrived)
  *   omega_combine          combine_results_optimized                   multi_resolution_fft.py:335-408
  *   omega_true_peak        ProfessionalMetering.calculate_true_peak    professional_meters.py:283-299
+ *   omega_true_peak_os     calculate_true_peak(x, oversampling)         professional_meters.py:283-299
  *   omega_k_weighting      ProfessionalMetering.apply_k_weighting      professional_meters.py:129-153
  *                          (+ the instantaneous LUFS of calculate_lufs :236-246)
  *   omega_meter_*          the momentary/short-term/integrated/range/true-peak deques  professional_meters.py:19-25, :248-279
@@ -144,6 +145,11 @@ int omega_combine(omega_ctx* ctx, const float* const* mags, int64_t n_cf, float*
 
 /* calculate_true_peak(x, 4) for n frames of length m (power of two 512..16384), contiguous. */
 int omega_true_peak(omega_ctx* ctx, const float* x, int64_t n, int32_t m, float* out_db, int mem);
+/* calculate_true_peak(x, oversampling) (professional_meters.py:283-299) for oversampling 1, 2 or 4:
+ * max |resample(x, oversampling * m)| over the phases n + p / oversampling; other factors return
+ * OMEGA_EUNSUP. */
+int omega_true_peak_os(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t oversampling, float* out_db,
+                       int mem);
 
 /* apply_k_weighting for n frames of length m (power of two 512..16384): weighted [n, m] (may be
  * NULL) and the instantaneous LUFS [n] (may be NULL). */

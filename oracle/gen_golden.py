@@ -46,6 +46,7 @@ def _import_reference():
     from omega4.panels.chromagram import ChromagramAnalyzer
     from omega4.optimization.batched_fft_processor import BatchedFFTProcessor
     from omega4.analyzers.drum_detection import EnhancedKickDetector, EnhancedSnareDetector
+    from omega4.optimization.gpu_accelerated_fft import GPUAcceleratedFFT
     return SimpleNamespace(**locals())
 
 
@@ -188,6 +189,81 @@ def gen_chroma(R):
     d["a440_mag"] = s
     d["a440_out"] = R.ChromagramAnalyzer(FS).compute_chromagram(s, freqs)
     np.savez_compressed(os.path.join(OUT, "chroma.npz"), **d)
+
+
+def metal_frames(n=16384):
+    """Blackman-windowed 16384-point magnitude frames of power chords on E2 (standard), Eb2 (half
+    step down) and D2 (drop D) bass notes with octave and fifth, a noise frame and a silent frame: the
+    tuning detection of chromagram.py:581-639 sees 0 / -1 / -2 and keeps its offset on frames without
+    a bass peak."""
+    rng = np.random.default_rng(21)
+    t = np.arange(n) / FS
+    w = np.blackman(n).astype(np.float32)
+
+    def chord(f0):
+        x = sum(a * np.sin(2 * np.pi * f0 * m * t) for m, a in ((1, 0.5), (1.5, 0.3), (2, 0.3), (3, 0.15)))
+        return (x + 0.01 * rng.standard_normal(n)).astype(np.float32)
+
+    seq = [73.42] * 6 + [82.41] * 3 + [77.78] * 7 + ["noise", "silence"] + [73.42] * 2
+    out = []
+    for f in seq:
+        if f == "noise":
+            x = (0.2 * rng.standard_normal(n)).astype(np.float32)
+        elif f == "silence":
+            x = np.zeros(n, np.float32)
+        else:
+            x = chord(f)
+        out.append(np.abs(np.fft.rfft(x * w)).astype(np.float32))
+    return np.stack(out)
+
+
+def gen_chroma_genre(R):
+    """compute_chromagram sequences with current_genre metal / rock (tuning offset per frame) and jazz
+    (blend 0.5), 16384-point spectra."""
+    d = {"versions": VERSIONS}
+    mags = metal_frames()
+    freqs = np.fft.rfftfreq(16384, 1 / FS)
+    d["mags"], d["freqs"] = mags, freqs
+    for genre in ("metal", "rock", "jazz"):
+        ca = R.ChromagramAnalyzer(FS)
+        ca.current_genre = genre
+        outs, offs = [], []
+        for m in mags:
+            outs.append(ca.compute_chromagram(m, freqs))
+            offs.append(ca.transposition_offset)
+        d[f"{genre}/out"] = np.stack(outs)
+        d[f"{genre}/offset"] = np.array(offs, np.int32)
+    np.savez_compressed(os.path.join(OUT, "chroma_genre.npz"), **d)
+
+
+def gen_gpufft(R):
+    """GPUAcceleratedFFT (gpu_accelerated_fft.py, CPU branch: CuPy is absent) -- compute_fft per
+    window and input dtype, its first-100-bytes cache, compute_multi_resolution_fft with a zero-padded
+    resolution."""
+    d = {"versions": VERSIONS}
+    g = R.GPUAcceleratedFFT()
+    cases = (("noise_4096_hann", S.noise(11, 4096, 0.2), "hann"),
+             ("comp_f64_2048_hamming", S.composite(2048).astype(np.float64), "hamming"),
+             ("triad_8192_blackman", S.triad(8192, 0.3), "blackman"),
+             ("sine_16384_hann", S.sine(997, 0.4, 16384), "hann"))
+    for name, x, w in cases:
+        mag, cp = g.compute_fft(x, w, return_complex=True)
+        d[f"fft/{name}/x"], d[f"fft/{name}/mag"], d[f"fft/{name}/complex"] = x, mag, cp
+    # the cache: a second signal with the same first 25 float32 samples returns the first's result
+    a = S.noise(12, 4096, 0.2)
+    b = a.copy()
+    b[100:] = S.noise(13, 4096 - 100, 0.2)
+    g2 = R.GPUAcceleratedFFT()
+    d["cache/a"], d["cache/b"] = a, b
+    d["cache/mag_a"] = g2.compute_fft(a, "hann")[0]
+    d["cache/mag_b"] = g2.compute_fft(b, "hann")[0]
+    x = S.noise(14, 6000, 0.2)
+    res = R.GPUAcceleratedFFT().compute_multi_resolution_fft(x, {"bass": 8192, "mid": 4096, "high": 1024}, "hann")
+    d["multi/x"] = x
+    for k, v in res.items():
+        for f in ("magnitude", "complex", "freqs"):
+            d[f"multi/{k}/{f}"] = v[f]
+    np.savez_compressed(os.path.join(OUT, "gpufft.npz"), **d)
 
 
 def gen_batched(R):
@@ -355,6 +431,6 @@ if __name__ == "__main__":
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post"))]:
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft"))]:
         g(R)
         print("wrote", g.__name__)

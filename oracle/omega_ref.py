@@ -523,16 +523,60 @@ def chroma_matrix(freqs: np.ndarray, offset: float = 0.0) -> np.ndarray:
     return M
 
 
+_TUNING_REFS = ((0, 82.41), (-1, 82.41 * 0.944), (-2, 82.41 * 0.891), (-3, 82.41 * 0.841), (-4, 82.41 * 0.794))
+
+
+def find_peaks_simple(data: np.ndarray, prominence: float = 0.3) -> List[int]:
+    """chromagram.py:641-654: strict interior local maxima above prominence * max."""
+    if len(data) < 3:
+        return []
+    thr = np.max(data) * prominence
+    return [i for i in range(1, len(data) - 1) if data[i] > data[i - 1] and data[i] > data[i + 1] and data[i] > thr]
+
+
+def detect_tuning_offset(fft: np.ndarray, freqs: np.ndarray, history: List[int], current: int) -> int:
+    """chromagram.py:581-639: the first peak of the 70-100 Hz bins against the E2 references within
+    50 cents (closest wins, 0 if none); the mode of the last 30 detections once there are 5
+    (Counter.most_common: first-inserted among equal counts). history is mutated."""
+    m = (freqs > 70) & (freqs < 100)
+    bass, bf = fft[m], freqs[m]
+    if len(bass) == 0:
+        return current
+    pk = find_peaks_simple(bass, 0.3)
+    if not pk:
+        return current
+    pf = bf[pk[0]]
+    best, dmin = 0, float("inf")
+    for off, rf in _TUNING_REFS:
+        if pf > 0 and rf > 0:
+            d = abs(1200 * np.log2(pf / rf))
+            if d < dmin and d < 50:
+                dmin, best = d, off
+    history.append(best)
+    if len(history) > 30:
+        history.pop(0)
+    if len(history) >= 5:
+        from collections import Counter
+        return Counter(history).most_common(1)[0][0]
+    return best
+
+
 class ChromaState:
-    """Per-stream chroma_history (chromagram.py:96) with the genre blend (:215-237)."""
+    """Per-stream chroma_history (chromagram.py:96) with the genre blend (:215-237) and, for metal /
+    rock, the per-frame tuning offset (:111-113, :128-129) -- an integer semitone shift of the pitch
+    map."""
 
     def __init__(self, genre: str = "pop"):
         self.hist = deque(maxlen=8)
         self.genre = genre
+        self.offset = 0
+        self.tuning_history: List[int] = []
 
     def compute(self, fft: np.ndarray, freqs: np.ndarray) -> np.ndarray:
+        if self.genre.lower() in ("metal", "rock"):
+            self.offset = detect_tuning_offset(fft, freqs, self.tuning_history, self.offset)
         enh = suppress_harmonics(np.asarray(fft).copy(), freqs)
-        chroma = chroma_matrix(freqs) @ enh.astype(np.float64)
+        chroma = chroma_matrix(freqs, self.offset) @ enh.astype(np.float64)
         sm = np.array([0.25 * chroma[(i - 1) % 12] + 0.5 * chroma[i] + 0.25 * chroma[(i + 1) % 12]
                        for i in range(12)])
         if np.sum(sm) > 0:
@@ -548,6 +592,16 @@ class ChromaState:
 # A13: BatchedFFTProcessor CPU branch   (omega4/optimization/batched_fft_processor.py:119-146,
 #      :269-285)
 # ----------------------------------------------------------------------------------------------
+
+
+def gpu_fft(audio: np.ndarray, window_type: str = "hann"):
+    """GPUAcceleratedFFT.compute_fft (gpu_accelerated_fft.py:92-177) without its prefix cache:
+    audio * window(n).astype(float32) (np.hanning / np.hamming / else np.blackman), rfft, |.|; the
+    arithmetic follows the input dtype (the CPU branch; the CuPy branch casts to float32)."""
+    n = len(audio)
+    w = {"hann": np.hanning, "hamming": np.hamming}.get(window_type, np.blackman)(n).astype(np.float32)
+    c = np.fft.rfft(audio * w)
+    return np.abs(c), c
 
 
 def batched_fft(audio: np.ndarray, fft_size: int, window_type: str = "hann", fs: float = 48000):

@@ -222,6 +222,24 @@ def test_meter_unsupported_length_keeps_state():
     assert pm.calculate_lufs(np.zeros(0, np.float32)) is pm.current_lufs
 
 
+@pytest.mark.parametrize("m", [1024, 8192, 16384])
+def test_true_peak_oversampling(m):
+    """calculate_true_peak(x, oversampling) for 1, 2 and 4 (phase subsets of the polyphase transform)
+    against scipy's resample (the oracle); an unsupported factor is logged and the previous value
+    returned; apply_weighting in an unimplemented mode logs and gives zeros (no exception)."""
+    from omega_gpu.professional_meters import ProfessionalMetering
+    pm = ProfessionalMetering(FS)
+    x = S.sine(997, 0.4, m) + S.noise(31, m, 0.05)
+    for o in (4, 2, 1):
+        got = pm.calculate_true_peak(x, o)
+        assert abs(got - R.true_peak(x, o)) < TP_TOL_DB, (m, o)
+    assert pm.calculate_true_peak(x, 4) > pm.calculate_true_peak(x, 2) - 1e-6 > pm.calculate_true_peak(x, 1) - 2e-6
+    prev = pm.calculate_true_peak(x, 4)
+    assert pm.calculate_true_peak(x, 3) == prev
+    pm.weighting_mode = "A"
+    assert not pm.apply_weighting(x).any()
+
+
 def test_bands_golden(golden):
     from omega_gpu.bands import PipelineBands, PrecomputedFrequencyMapper
     g = golden("bands")
@@ -256,6 +274,60 @@ def test_chroma_golden(golden):
     a = ChromagramAnalyzer(FS).compute_chromagram(g["a440_mag"], g["freqs"])
     assert int(np.argmax(a)) == 9
     np.testing.assert_allclose(a, g["a440_out"], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("genre", ["metal", "rock", "jazz"])
+def test_chroma_genre_golden(golden, genre):
+    """Metal / rock tuning offsets (drop D, E, Eb; the 30-deep mode) and the jazz blend against the
+    reference's own sequences; per frame and batched."""
+    from omega_gpu.chromagram import ChromagramAnalyzer
+    g = golden("chroma_genre")
+    ca = ChromagramAnalyzer(FS)
+    ca.current_genre = genre
+    out, offs = [], []
+    for m in g["mags"]:
+        out.append(ca.compute_chromagram(m, g["freqs"]))
+        offs.append(ca.transposition_offset)
+    np.testing.assert_array_equal(offs, g[f"{genre}/offset"])
+    np.testing.assert_allclose(np.stack(out), g[f"{genre}/out"], rtol=1e-6, atol=1e-9)
+    cb = ChromagramAnalyzer(FS)
+    cb.current_genre = genre
+    np.testing.assert_allclose(cb.compute_chromagram_batch(g["mags"], g["freqs"]), g[f"{genre}/out"],
+                               rtol=1e-6, atol=1e-9)
+
+
+def test_gpu_accelerated_fft_golden(golden):
+    """GPUAcceleratedFFT facade: compute_fft per window and input dtype (float32 device transform vs
+    the reference's CPU branch, 1e-4 normwise), its first-100-bytes cache, the multi-resolution
+    dict with a zero-padded size, process_fft_batch on device tensors, unsupported sizes logged."""
+    import torch
+    from omega_gpu.gpu_accelerated_fft import GPUAcceleratedFFT
+    g = golden("gpufft")
+    ga = GPUAcceleratedFFT()
+    for name, w in (("noise_4096_hann", "hann"), ("comp_f64_2048_hamming", "hamming"),
+                    ("triad_8192_blackman", "blackman"), ("sine_16384_hann", "hann")):
+        mag, cp = ga.compute_fft(g[f"fft/{name}/x"], w)
+        assert normwise(mag, g[f"fft/{name}/mag"]) < SPEC_TOL, name
+        assert np.abs(cp - g[f"fft/{name}/complex"]).max() / np.abs(g[f"fft/{name}/complex"]).max() < SPEC_TOL
+    gc = GPUAcceleratedFFT()
+    ma = gc.compute_fft(g["cache/a"], "hann")[0]
+    mb = gc.compute_fft(g["cache/b"], "hann")[0]
+    assert mb is ma  # the reference's prefix cache: the same cached spectrum
+    assert normwise(mb, g["cache/mag_b"]) < SPEC_TOL
+    res = GPUAcceleratedFFT().compute_multi_resolution_fft(g["multi/x"], {"bass": 8192, "mid": 4096, "high": 1024})
+    for k in ("bass", "mid", "high"):
+        assert normwise(res[k]["magnitude"], g[f"multi/{k}/magnitude"]) < SPEC_TOL, k
+        np.testing.assert_array_equal(res[k]["freqs"], g[f"multi/{k}/freqs"])
+    inp, _ = ga.prepare_batch_arrays(3, 4096)
+    x = np.stack([S.noise(s, 4096, 0.2) for s in (1, 2, 3)])
+    inp.copy_(torch.from_numpy(x))
+    out = ga.process_fft_batch(inp, "hamming")
+    assert out.is_cuda and out.dtype == torch.complex64 and out.shape == (3, 2049)
+    ref = np.stack([R.gpu_fft(r, "hamming")[1] for r in x])
+    assert np.abs(out.cpu().numpy() - ref).max() / np.abs(ref).max() < SPEC_TOL
+    assert ga.process_fft_batch(torch.zeros((2, 3000), device="cuda")) is None  # logged, not raised
+    mag, _ = ga.compute_fft(np.ones(3000, np.float32))
+    assert mag.shape == (1501,) and not mag.any()
 
 
 def test_batched_fft_golden(golden):

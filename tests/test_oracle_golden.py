@@ -170,6 +170,40 @@ def test_chroma(golden):
     assert int(np.argmax(a)) == 9  # A
 
 
+@pytest.mark.parametrize("genre", ["metal", "rock", "jazz"])
+def test_chroma_genre(golden, genre):
+    """compute_chromagram with current_genre metal / rock (per-frame tuning offset: drop D, E, Eb and
+    the 30-deep mode with its first-inserted tie break) and jazz (blend 0.5), 16384-point spectra."""
+    g = golden("chroma_genre")
+    st = R.ChromaState(genre)
+    out, offs = [], []
+    for m in g["mags"]:
+        out.append(st.compute(m, g["freqs"]))
+        offs.append(st.offset)
+    np.testing.assert_array_equal(offs, g[f"{genre}/offset"])
+    np.testing.assert_allclose(np.stack(out), g[f"{genre}/out"], rtol=1e-10, atol=1e-14)
+    if genre != "jazz":
+        assert set(offs) == {-2, -1}
+
+
+def test_gpu_accelerated_fft(golden):
+    """GPUAcceleratedFFT.compute_fft / compute_multi_resolution_fft (reference CPU branch) against the
+    restatement; the reference's first-100-bytes cache returns the first signal's spectrum."""
+    g = golden("gpufft")
+    for name, w in (("noise_4096_hann", "hann"), ("comp_f64_2048_hamming", "hamming"),
+                    ("triad_8192_blackman", "blackman"), ("sine_16384_hann", "hann")):
+        mag, cp = R.gpu_fft(g[f"fft/{name}/x"], w)
+        np.testing.assert_array_equal(mag, g[f"fft/{name}/mag"])
+        np.testing.assert_array_equal(cp, g[f"fft/{name}/complex"])
+    np.testing.assert_array_equal(g["cache/mag_b"], g["cache/mag_a"])
+    assert not np.array_equal(R.gpu_fft(g["cache/b"])[0], g["cache/mag_b"])
+    x = g["multi/x"]
+    for k, n in (("bass", 8192), ("mid", 4096), ("high", 1024)):
+        chunk = x[-n:] if len(x) >= n else np.pad(x, (0, n - len(x)))
+        np.testing.assert_array_equal(R.gpu_fft(chunk)[0], g[f"multi/{k}/magnitude"])
+        np.testing.assert_array_equal(np.fft.rfftfreq(n, 1 / 48000), g[f"multi/{k}/freqs"])
+
+
 def test_batched(golden):
     g = golden("batched")
     for name, n, w in (("app_f64_2048_hann", 2048, "hann"), ("f32_4096_blackman", 4096, "blackman"),
