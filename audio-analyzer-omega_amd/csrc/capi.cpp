@@ -1236,6 +1236,15 @@ int omega_set_stream(omega_ctx* c, void* s) {
   return 0;
 }
 
+void* omega_get_stream(const omega_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+int omega_get_config(const omega_ctx* c, omega_config* cfg, int* device) {
+  if (!c) return OMEGA_EINVAL;
+  if (cfg) *cfg = c->cfg;
+  if (device) *device = c->device;
+  return 0;
+}
+
 int omega_set_graphs(omega_ctx* c, int enable) {
   if (!c) return OMEGA_EINVAL;
   c->use_graph = (enable & 1) != 0;

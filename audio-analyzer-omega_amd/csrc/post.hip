@@ -12,11 +12,14 @@
 // np.intp count and rounded to float32).
 //
 // Bit-exactness needs every float32 operation rounded on its own: floating-point contraction is off
-// for this file (HIP's default -ffp-contract=fast fused the percentile's lerp into an FMA, 1 ulp off
-// the reference's reference value on some frames -- then every bin of such a frame).
+// for this file, and the arithmetic is written with plain operators -- HIP's __fmul_rn / __fsub_rn
+// come from the device library with contraction allowed, and the backend still fused the
+// percentile's lerp into an FMA (1 ulp off the reference value on the last golden frame, then every
+// bin of that frame).
 //   post_frame_kernel: one 256-thread workgroup per frame (independent frames).
 //   post_ema_kernel: one workgroup, one thread per band, the frames in order (the EMA recurrence).
 #include "fft.hpp"
+#include "numpy_emul.hpp"
 #include "params.hpp"
 
 #pragma clang fp contract(off)
@@ -38,48 +41,6 @@ __device__ __forceinline__ T block_reduce(T v, T* red, int t, Op op) {
 #pragma unroll
   for (int w = 1; w < kPostThreads / 64; ++w) r = op(r, red[w]);
   return r;
-}
-
-// numpy's pairwise_sum for contiguous float32 (numpy/_core/src/umath/loops_utils.h.src): below 8
-// elements a plain running sum, up to 128 eight interleaved accumulators combined as
-// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) plus the tail, above that the two halves split at a
-// multiple of 8 below n / 2. np.add.reduce starts from the identity 0 (0 + s == s).
-__device__ __noinline__ float np_pairwise_leaf(const float* a, int n) {
-  if (n < 8) {
-    float r = 0.f;
-    for (int i = 0; i < n; ++i) r += a[i];
-    return r;
-  }
-  float r[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = a[j];
-  int i = 8;
-  for (; i < n - (n % 8); i += 8) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
-  }
-  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-  for (; i < n; ++i) res += a[i];
-  return res;
-}
-
-template <int D>
-__device__ float np_pairwise_sum(const float* a, int n) {
-  if constexpr (D == 0) {
-    return np_pairwise_leaf(a, n);
-  } else {
-    if (n <= 128) return np_pairwise_leaf(a, n);
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    return np_pairwise_sum<D - 1>(a, n2) + np_pairwise_sum<D - 1>(a + n2, n - n2);
-  }
-}
-
-// np.mean of a float32 range: float32(float64(pairwise sum) / float64(n)) (_methods._mean divides the
-// float32 sum by an np.intp count, which promotes to float64)
-__device__ __forceinline__ float np_mean_f32(const float* a, int n) {
-  static_assert(kPostMaxBins <= 128 << 5, "pairwise recursion depth");
-  return (float)((double)np_pairwise_sum<5>(a, n) / (double)n);
 }
 
 }  // namespace
@@ -155,9 +116,9 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
     __syncthreads();
     const float a = pv[0], b = pv[1], d = b - a;
     // numpy _lerp, no contraction
-    const float ref = p.p_g >= 0.5f ? __fsub_rn(b, __fmul_rn(d, 1.0f - p.p_g)) : __fadd_rn(a, __fmul_rn(d, p.p_g));
+    const float ref = p.p_g >= 0.5f ? b - d * (1.0f - p.p_g) : a + d * p.p_g;
     if (ref > 0.f)
-      for (int i = t; i < T; i += kPostThreads) s[i] = __fmul_rn(__fdiv_rn(s[i], ref), 0.8f);
+      for (int i = t; i < T; i += kPostThreads) s[i] = s[i] / ref * 0.8f;
   }
   // 4) frequency compensation (factors by position) and 5) optional max normalisation
   const float* comp = p.comp[content == 1 ? 1 : 0];
@@ -169,7 +130,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
     for (int i = t; i < T; i += kPostThreads) m = fmaxf(m, s[i]);
     m = block_reduce(m, redf, t, fmx);
     if (m > 0.f && !has_nan)
-      for (int i = t; i < T; i += kPostThreads) s[i] = __fdiv_rn(s[i], m);
+      for (int i = t; i < T; i += kPostThreads) s[i] = s[i] / m;
     __syncthreads();
   }
   for (int i = t; i < T; i += kPostThreads) p.spec_out[f * T + i] = s[i];
@@ -199,7 +160,7 @@ __global__ __launch_bounds__(kPostMaxBands) void post_ema_kernel(PostParams p) {
     bool have = had;
     for (int64_t f = 0; f < p.n; ++f) {
       float v = p.band_out[f * p.nb + b];
-      if ((p.flags & 8) && have) v = __fadd_rn(__fmul_rn(prev, sf), __fmul_rn(v, sf1));
+      if ((p.flags & 8) && have) v = prev * sf + v * sf1;
       p.band_out[f * p.nb + b] = v;
       prev = v;
       have = true;

@@ -40,6 +40,22 @@ class Outputs(C.Structure):
                 ("meters", C.c_void_p), ("mag", C.c_void_p * MAX_RES), ("weighted", C.c_void_p)]
 
 
+class IngestConfig(C.Structure):
+    _fields_ = [("format", C.c_int32), ("sample_rate", C.c_int32), ("hop", C.c_int32), ("batch_hops", C.c_int32),
+                ("ring_slots", C.c_int32), ("max_pending_batches", C.c_int32), ("chunk_size", C.c_int32), ("gain", C.c_float), ("gate", C.c_int32),
+                ("noise_floor", C.c_double), ("silence_threshold_seconds", C.c_double),
+                ("background_alpha", C.c_double), ("want", C.c_int32)]
+
+
+class IngestStats(C.Structure):
+    _fields_ = [("bytes_in", C.c_int64), ("batches", C.c_int64), ("frames", C.c_int64),
+                ("frames_polled", C.c_int64), ("dropped_frames", C.c_int64)]
+
+
+FMT = {"float32le": 0, "s16le": 1}
+INGEST_COMBINED, INGEST_LUFS, INGEST_TRUE_PEAK, INGEST_METERS = 1, 2, 4, 8
+
+
 class OmegaError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"libomega error {code}: {msg}")
@@ -58,6 +74,16 @@ EXPORTS = {
     "omega_last_error": (C.c_char_p, [C.c_void_p]),
     "omega_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "omega_synchronize": (C.c_int, [C.c_void_p]),
+    "omega_get_stream": (C.c_void_p, [C.c_void_p]),
+    "omega_get_config": (C.c_int, [C.c_void_p, C.POINTER(Config), C.POINTER(C.c_int)]),
+    "omega_ingest_config_default": (None, [C.POINTER(IngestConfig)]),
+    "omega_ingest_create": (C.c_int, [C.c_void_p, C.POINTER(IngestConfig), C.POINTER(C.c_void_p)]),
+    "omega_ingest_push": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+    "omega_ingest_flush": (C.c_int, [C.c_void_p]),
+    "omega_ingest_poll": (C.c_int, [C.c_void_p, C.c_int64, C.POINTER(Outputs), C.c_int, C.POINTER(C.c_int64)]),
+    "omega_ingest_get_stats": (C.c_int, [C.c_void_p, C.POINTER(IngestStats)]),
+    "omega_ingest_last_error": (C.c_char_p, [C.c_void_p]),
+    "omega_ingest_destroy": (None, [C.c_void_p]),
     "omega_set_graphs": (C.c_int, [C.c_void_p, C.c_int]),
     "omega_process_frames": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int64,
                                        C.POINTER(Outputs), C.c_int]),

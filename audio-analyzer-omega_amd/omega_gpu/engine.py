@@ -76,6 +76,7 @@ class Engine:
         self.resolutions = tuple(resolutions)
         self.W, self.C, self.T = cfg.frame_size, cfg.n_channels, cfg.target_bins
         self.device = device
+        self._ingests = []  # weak references: stream ingests bound to this context, closed before it
         code = lib.omega_create(C.byref(cfg), int(device), C.byref(self._ctx))
         if code != L.OK:
             msg = lib.omega_last_error(self._ctx).decode()
@@ -87,6 +88,10 @@ class Engine:
 
     # -- lifecycle --
     def close(self):
+        for r in getattr(self, "_ingests", ()):
+            ing = r()
+            if ing is not None:
+                ing.close()
         if self._ctx:
             L.lib().omega_destroy(self._ctx)
             self._ctx = C.c_void_p()

@@ -127,6 +127,9 @@ int omega_set_stream(omega_ctx* ctx, void* hip_stream);
  * peak / K-weighting + meters); 3 the full-chip kernels back to back on the stream, the latency-bound
  * meter prep and LUFS query kernels on a side stream joined by events. */
 int omega_set_graphs(omega_ctx* ctx, int flags);
+/* The stream calls enqueue on (omega_set_stream), and the context's configuration and device. */
+void* omega_get_stream(const omega_ctx* ctx);
+int omega_get_config(const omega_ctx* ctx, omega_config* cfg, int* device);
 int omega_synchronize(omega_ctx* ctx);
 
 /* The fused per-channel-frame hot path over n_frames x n_channels frames of W samples. */
@@ -239,6 +242,59 @@ int omega_post_process(omega_ctx* ctx, const float* spectra, int64_t n_frames, i
 int omega_post_reset(omega_ctx* ctx);
 int omega_spectra(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t window, omega_bands* bands,
                   float* bands_out, double* chroma_out, float* mag_out, int mem);
+
+
+/* ---- Sustained-stream ingest ------------------------------------------
+ * The capture byte stream of omega4/audio/capture.py:546-600 (parec float32le / s16le, fixed chunks
+ * of chunk_size samples, s16 scaled by 1/32768), its per-chunk noise gate (:620-641: RMS, background
+ * EMA, silence counter -> zeros) and the app's input gain + ring buffer (omega4_main.py:648-688),
+ * feeding omega_process_stream: frame f of every channel covers stream samples [f*hop, f*hop + W).
+ * Bytes are interleaved over the context's n_channels. omega_ingest_push memcpy's them into
+ * page-locked staging slots; each full slot (batch_hops * hop samples per channel) is copied to the
+ * device on a copy stream and analysed on the ingest's compute stream (bound to the context with
+ * omega_set_stream; destroy the ingest before the context, and before using the context directly
+ * again), overlapping the next slot's copy. push blocks only while the slot it fills is still being
+ * copied to the device. Results come back through omega_ingest_poll in frame order; when
+ * max_pending_batches batches wait unpolled, the oldest one's frames are dropped and counted (the
+ * capture buffer's drop policy, capture.py:579-580). */
+typedef enum { OMEGA_FMT_F32LE = 0, OMEGA_FMT_S16LE = 1 } omega_sample_format;
+enum { OMEGA_INGEST_COMBINED = 1, OMEGA_INGEST_LUFS = 2, OMEGA_INGEST_TRUE_PEAK = 4, OMEGA_INGEST_METERS = 8 };
+
+typedef struct {
+  int32_t format;                   /* omega_sample_format */
+  int32_t sample_rate;              /* for the gate's silence threshold (capture.py:227) */
+  int32_t hop;                      /* frame hop H, multiple of 4 */
+  int32_t batch_hops;               /* hops per device batch; batch_hops * hop % chunk_size == 0 */
+  int32_t ring_slots;               /* page-locked input staging slots, >= 2 */
+  int32_t max_pending_batches;      /* result blocks kept until polled (>= 2); beyond, the oldest drop */
+  int32_t chunk_size;               /* capture chunk (noise-gate block), 1..8192 (capture.py:28, :64) */
+  float gain;                       /* input_gain (omega4_main.py:152, :660) */
+  int32_t gate;                     /* apply the capture noise gate */
+  double noise_floor;               /* 0.001 (capture.py:36) */
+  double silence_threshold_seconds; /* 0.25 */
+  double background_alpha;          /* 0.001 */
+  int32_t want;                     /* OMEGA_INGEST_* outputs */
+} omega_ingest_config;
+
+typedef struct {
+  int64_t bytes_in, batches, frames, frames_polled, dropped_frames;
+} omega_ingest_stats;
+
+typedef struct omega_ingest omega_ingest;
+
+void omega_ingest_config_default(omega_ingest_config* cfg);
+/* On an error after allocation *out is set: read omega_ingest_last_error, then omega_ingest_destroy. */
+int omega_ingest_create(omega_ctx* ctx, const omega_ingest_config* cfg, omega_ingest** out);
+int omega_ingest_push(omega_ingest* in, const void* bytes, int64_t n_bytes);
+/* Analyse the whole chunks buffered so far (the rest stays buffered). */
+int omega_ingest_flush(omega_ingest* in);
+/* Up to max_frames completed frames (per channel) in frame order into host buffers laid out like
+ * omega_outputs ([frames * C, T], [frames * C], [frames * C, 5]; NULL pointers skip); wait != 0
+ * blocks until the launched batches are done. */
+int omega_ingest_poll(omega_ingest* in, int64_t max_frames, const omega_outputs* out, int wait, int64_t* n_frames_out);
+int omega_ingest_get_stats(const omega_ingest* in, omega_ingest_stats* out);
+const char* omega_ingest_last_error(const omega_ingest* in);
+void omega_ingest_destroy(omega_ingest* in);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,7 @@ def _import_reference():
     from omega4.optimization.batched_fft_processor import BatchedFFTProcessor
     from omega4.analyzers.drum_detection import EnhancedKickDetector, EnhancedSnareDetector
     from omega4.optimization.gpu_accelerated_fft import GPUAcceleratedFFT
+    from omega4.audio.capture import AudioCaptureConfig, PipeWireMonitorCapture
     return SimpleNamespace(**locals())
 
 
@@ -266,6 +267,42 @@ def gen_gpufft(R):
     np.savez_compressed(os.path.join(OUT, "gpufft.npz"), **d)
 
 
+def capture_signal(n_chunks=240, chunk=512, seed=31):
+    """float32 capture chunks: music-level tone + noise, a fade into near-silence held past the 0.25 s
+    silence threshold, a noise floor between the gate floor and twice it (the background EMA
+    updates), a loud burst, and an exact-zero stretch."""
+    rng = np.random.default_rng(seed)
+    n = n_chunks * chunk
+    t = np.arange(n) / FS
+    x = 0.3 * np.sin(2 * np.pi * 220 * t) + 0.02 * rng.standard_normal(n)
+    env = np.ones(n)
+    env[40 * chunk:50 * chunk] = np.linspace(1, 1e-4, 10 * chunk)
+    env[50 * chunk:90 * chunk] = 1e-4
+    x[90 * chunk:130 * chunk] = 0.0015 * rng.standard_normal(40 * chunk)
+    env[90 * chunk:130 * chunk] = 1
+    x[130 * chunk:150 * chunk] *= 3
+    x[200 * chunk:220 * chunk] = 0
+    return (x * env).astype(np.float32)
+
+
+def gen_capture(R):
+    """PipeWireMonitorCapture._process_audio_frame (capture.py:620-641) chunk by chunk on one capture
+    object with the default config (no process is started): outputs, background level and silence
+    counter after each chunk."""
+    d = {"versions": VERSIONS}
+    cap = R.PipeWireMonitorCapture("golden", R.AudioCaptureConfig())
+    x = capture_signal()
+    outs, bg, sil = [], [], []
+    for k in range(len(x) // 512):
+        outs.append(np.array(cap._process_audio_frame(x[k * 512:(k + 1) * 512])))
+        bg.append(float(cap.background_level))
+        sil.append(cap.silence_samples)
+    d["x"], d["out"] = x, np.concatenate(outs).astype(np.float32)
+    d["bg"], d["silence"] = np.array(bg), np.array(sil, np.int64)
+    d["bg_type"] = np.array([type(cap.background_level).__name__])
+    np.savez_compressed(os.path.join(OUT, "capture.npz"), **d)
+
+
 def gen_batched(R):
     d = {"versions": VERSIONS}
     bp = R.BatchedFFTProcessor()
@@ -431,6 +468,6 @@ if __name__ == "__main__":
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft"))]:
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture"))]:
         g(R)
         print("wrote", g.__name__)

@@ -837,3 +837,49 @@ def app_post_sequence(combined: np.ndarray, comb_freqs, **kw):
     out = [st.update(c) for c in combined]
     return (np.stack([o[0] for o in out]), np.stack([o[1] for o in out]).astype(np.float64),
             np.array([o[2] for o in out], np.int32))
+
+
+# ----------------------------------------------------------------------------------------------
+# the capture stream before the path -- parec chunks, the per-chunk noise
+# gate (omega4/audio/capture.py:546-600, :620-641) and the app's input gain (omega4_main.py:648-688)
+# ----------------------------------------------------------------------------------------------
+
+
+class CaptureGate:
+    """PipeWireMonitorCapture._process_audio_frame (capture.py:620-641) with AudioCaptureConfig's
+    defaults (:28, :36-39). The expressions keep numpy's types: the RMS is a float32 scalar, so the
+    background level turns float32 at its first update (Python float times np.float32)."""
+
+    def __init__(self, fs: int = 48000, chunk: int = 512, noise_floor: float = 0.001,
+                 silence_threshold_seconds: float = 0.25, background_alpha: float = 0.001):
+        self.chunk, self.noise_floor, self.alpha = chunk, noise_floor, background_alpha
+        self.silence_samples = 0
+        self.silence_threshold = int(fs * silence_threshold_seconds)
+        self.background_level = 0.0
+
+    def process(self, x: np.ndarray) -> np.ndarray:
+        rms = np.sqrt(np.mean(x ** 2))
+        if rms < self.noise_floor * 2:
+            self.background_level = (1 - self.alpha) * self.background_level + self.alpha * rms
+        if rms < max(self.noise_floor, self.background_level * 3):
+            self.silence_samples += self.chunk
+            if self.silence_samples > self.silence_threshold:
+                return np.zeros_like(x)
+        else:
+            self.silence_samples = 0
+        return x
+
+
+def capture_stream(x: np.ndarray, fs: int = 48000, chunk: int = 512, gain: float = 4.0, gate: bool = True) -> np.ndarray:
+    """One channel's analysed stream: whole capture chunks through the gate, times input_gain
+    (float32 array times a Python float stays float32)."""
+    g = CaptureGate(fs, chunk)
+    n = len(x) // chunk * chunk
+    y = np.concatenate([g.process(x[i:i + chunk]) if gate else x[i:i + chunk] for i in range(0, n, chunk)]) \
+        if n else np.zeros(0, np.float32)
+    return y * gain
+
+
+def s16le_samples(data: bytes) -> np.ndarray:
+    """capture.py:571-574 for s16le: int16 -> float32 / 32768.0."""
+    return np.frombuffer(data, dtype=np.int16).astype(np.float32) / 32768.0

@@ -76,3 +76,11 @@ def level_steps(frames: int, m: int, seed: int = 3) -> np.ndarray:
         ph = (f // 37) % 5
         lv[f] = (0.3, 0.03, 0.0, 0.0001, 0.9)[ph] * (1 + 0.1 * rng.random())
     return (base * lv[:, None]).astype(np.float32)
+
+
+def cfg5_stream(n: int, channels: int = 8, fs: float = 96000) -> np.ndarray:
+    """BASELINE cfg5 surround stream, planar [C, n] float32: channel c =
+    0.2 sin(2 pi 110 (c + 1) t) + 0.02 N(0, 1) (seed c)."""
+    t = np.arange(n) / fs
+    return np.stack([(0.2 * np.sin(2 * np.pi * 110 * (c + 1) * t)).astype(np.float32) + noise(c, n, 0.02)
+                     for c in range(channels)]).astype(np.float32)

@@ -241,3 +241,23 @@ def test_app_post(name):
     np.testing.assert_array_equal(b, g[f"{name}/bands"])
     np.testing.assert_array_equal(c, g[f"{name}/content"])
     assert set(c.tolist()) >= {1, 2}
+
+
+def test_capture_gate(golden):
+    """The capture noise gate (golden: the reference's own _process_audio_frame, chunk by chunk): the
+    gated chunks, the background level (float32 after its first update) and the silence counter."""
+    g = golden("capture")
+    gate = R.CaptureGate()
+    x = g["x"]
+    outs, bg, sil = [], [], []
+    for k in range(len(x) // 512):
+        outs.append(gate.process(x[k * 512:(k + 1) * 512]))
+        bg.append(float(gate.background_level))
+        sil.append(gate.silence_samples)
+    np.testing.assert_array_equal(np.concatenate(outs), g["out"])
+    np.testing.assert_array_equal(bg, g["bg"])
+    np.testing.assert_array_equal(sil, g["silence"])
+    assert type(gate.background_level).__name__ == str(g["bg_type"][0])
+    gated = (g["out"].reshape(-1, 512) == 0).all(axis=1) & (x.reshape(-1, 512) != 0).any(axis=1)
+    assert gated.sum() >= 15  # chunks the gate zeroed (besides the exact-zero stretch)
+    np.testing.assert_array_equal(R.capture_stream(x, gain=4.0), g["out"] * np.float32(4.0))
