@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 / drums / app_post lines")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 per-GPU-shard line")
     ap.add_argument("--cfg4-steps", type=int, default=20)
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 sustained-stream line")
+    ap.add_argument("--cfg5-seconds", type=float, default=60.0)
     # test hooks (tests/test_bench_launch.py): a stand-in compute backend on the CPU over gloo, a
     # smaller per-rank batch, and rank 0 dumping the last gathered blocks
     ap.add_argument("--standin", default=None, help=argparse.SUPPRESS)
@@ -76,6 +78,15 @@ def cfg2_input(frames=FRAMES, w=W, seed_l=0, seed_r=1):
     right = (0.25 * np.sin(2 * np.pi * 997 * t)).astype(np.float32) + \
         (0.05 * np.random.default_rng(seed_r).standard_normal(n)).astype(np.float32)
     return np.stack([left.reshape(frames, w), right.reshape(frames, w)], axis=1).astype(np.float32)
+
+
+def cfg5_input(n, channels=8, fs=96000):
+    """BASELINE cfg5 surround stream, planar [C, n]: channel c = 0.2 sin(2 pi 110 (c + 1) t)
+    + 0.02 N(0, 1) (seed c). Same formula as oracle/signals.cfg5_stream (tests/test_bench_contract.py)."""
+    t = np.arange(n) / fs
+    return np.stack([(0.2 * np.sin(2 * np.pi * 110 * (c + 1) * t)).astype(np.float32) +
+                     (0.02 * np.random.default_rng(c).standard_normal(n)).astype(np.float32)
+                     for c in range(channels)]).astype(np.float32)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -334,6 +345,63 @@ def post_line(dev, reps=20, n=4096, bins=512):
                          "bytes_per_frame": bpf}}
 
 
+def cfg5_line(rank, world, dev, seconds=60.0):
+    """BASELINE cfg5, the sustained stream: 96 kHz 8-channel surround, 60 s (SURVEY.md §8(d) signal),
+    pushed as interleaved float32le capture bytes in 512-sample chunks through the ingest
+    (omega_ingest_*: page-locked staging, async H2D, capture noise gate, stream layout), 16384-point
+    frames every 1024 samples with 4x true peak, K-weighted LUFS and the meter aggregates (integrated
+    window 3600 frames, reached at 38 s). One channel per GPU: rank r takes channels r, r + N, ...
+    Wall time from the first push to the last result polled on the host, so it includes the host
+    push, PCIe both ways and the analysis; max over ranks."""
+    from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
+    from omega_gpu.ingest import StreamIngest
+    fs, C_all, W5, H5 = 96000, 8, 16384, 1024
+    chans = list(range(rank, C_all, world))
+    n = int(fs * seconds)
+    x = cfg5_input(n, C_all, fs)[chans]
+    inter = np.ascontiguousarray(x.T)
+    eng = Engine(NORTHSTAR_RESOLUTIONS, fs, 20000, target_bins=T, n_channels=len(chans), device=dev.index or 0)
+    ing = StreamIngest(eng, hop=H5, batch_hops=64, ring_slots=4, gain=1.0)
+    # warm-up: one batch through a separate ingest
+    w = StreamIngest(Engine(NORTHSTAR_RESOLUTIONS, fs, 20000, target_bins=T, n_channels=len(chans),
+                            device=dev.index or 0), hop=H5, batch_hops=64)
+    w.push(inter[:W5 + 64 * H5])
+    w.flush()
+    w.poll(wait=True)
+    w.close()
+    frames = 0
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(0, n, 512):
+        ing.push(inter[i:i + 512])
+        if (i // 512) % 128 == 127:
+            frames += len(ing.poll()["lufs_inst"])
+    ing.flush()
+    got = ing.poll(wait=True)
+    frames += len(got["lufs_inst"])
+    dt = time.perf_counter() - t0
+    meters = got["meters"]
+    st = ing.stats()
+    ing.close()
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([dt, frames], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        dt, frames = float(tt[0]), int(tt[1])
+    per_ch = (n - W5) // H5 + 1
+    return {"workload": f"cfg5: 96 kHz x {C_all} ch x {seconds:.0f} s sustained stream, float32le capture bytes in "
+                        "512-sample chunks -> ingest (page-locked staging, async H2D, noise gate) -> 16384-pt frames "
+                        f"every {H5} samples (MRFFT 16k/8k/4k/1k + combine(512) + K-LUFS + 4x TP + meters, "
+                        "integrated window 3600 frames); one channel per GPU",
+            "value": frames / dt, "unit": "channel-frames/s", "wall_s": dt, "channel_frames": frames,
+            "expected_channel_frames": per_ch * C_all, "dropped_frames": st["dropped_frames"],
+            "realtime_factor": seconds / dt, "integrated_reached": bool(np.all(meters[-len(chans):, 2] > -100)),
+            "note": "host push + PCIe H2D/D2H + analysis, wall-clock on the host (not the HBM-resident headline)"}
+
+
 def cfg3_input(n, m):
     """BASELINE cfg3 synthetic frames (same generator as oracle/signals.cfg3_batch): even frames a
     0.5-amplitude C-major triad, odd frames 0.1 N(0,1) (seed 1234)."""
@@ -505,6 +573,9 @@ def main(argv=None):
                     "value": ncf4 * world * a.cfg4_steps / dt4, "unit": "channel-frames/s",
                     "ms_per_step": dt4 / a.cfg4_steps * 1e3, "steps": a.cfg4_steps,
                     "channel_frames_per_gpu": ncf4, "global_stereo_frames": FRAMES_CFG4 * world}
+    cfg5 = None
+    if not standin and not a.no_cfg5:
+        cfg5 = cfg5_line(rank, world, be.dev, a.cfg5_seconds)
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu_baseline and not standin:
@@ -528,6 +599,8 @@ def main(argv=None):
             line["backend"] = f"stand-in {a.standin} (CPU, {be.dist_backend}); not a measurement"
         if cfg4 is not None:
             line["cfg4"] = cfg4
+        if cfg5 is not None:
+            line["cfg5"] = cfg5
         if world == 1 and not a.no_cfg3 and not standin:
             line["cfg3"] = cfg3_line(be.dev)
             line["drums"] = drums_line(be.dev)

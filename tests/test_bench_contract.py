@@ -21,3 +21,9 @@ def test_cfg3_input_matches_oracle_generator():
     import bench
     from oracle import signals as S
     np.testing.assert_array_equal(bench.cfg3_input(8, 8192), S.cfg3_batch(8))
+
+
+def test_cfg5_input_matches_oracle_generator():
+    import bench
+    from oracle import signals as S
+    np.testing.assert_array_equal(bench.cfg5_input(5000, 8, 96000), S.cfg5_stream(5000, 8, 96000))
