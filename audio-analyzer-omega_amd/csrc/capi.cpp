@@ -41,6 +41,8 @@ hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int h
                          hipStream_t s);
 hipError_t launch_combine(const CombineParams& p, hipStream_t s);
 hipError_t launch_drum(const DrumParams& p, hipStream_t s);
+hipError_t launch_vu(const VuParams& p, hipStream_t s);
+hipError_t launch_transients(const TransientParams& p, hipStream_t s);
 hipError_t launch_post(const PostParams& p, hipStream_t s);
 hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s);
 }  // namespace omega
@@ -237,6 +239,15 @@ struct omega_ctx {
   long long* d_dpos[2] = {};
   float* d_dflux = nullptr;
   PostParams post{};  // omega_post_configure's tables (post.n_bins = 0: not configured)
+  // VU meter state (omega_vu_update), double-buffered: sample history, display / peak / hold time
+  double* d_vu_hist[2] = {};
+  double* d_vu_st[2] = {};
+  double* d_vu_ms = nullptr;
+  int64_t vu_ms_cap = 0, vu_total = 0;
+  int vu_cur = 0;
+  // transient-analysis tables per frame length: twiddles (float64) and the Savitzky-Golay weights
+  std::map<int, std::pair<double2*, double2*>> tr_tw;
+  double* d_sg = nullptr;
   int64_t dflux_cap = 0;
   // meter state (double-buffered)
   float* d_hist_l[2] = {};
@@ -1011,6 +1022,174 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   if (!e) e = build_meter_state(c);
   *out = c;
   return e;
+}
+
+int omega_vu_reset(omega_ctx* c) {
+  if (!c) return OMEGA_EINVAL;
+  c->vu_total = 0;
+  if (!c->d_vu_st[0]) return 0;
+  HIPC(c, hipSetDevice(c->device));
+  const int C = c->cfg.n_channels;
+  std::vector<double> st((size_t)C * 3);
+  for (int i = 0; i < C; ++i) {  // vu_meters.py:33-42: display and peak at -60, hold time 0
+    st[i * 3] = -60.0;
+    st[i * 3 + 1] = -60.0;
+    st[i * 3 + 2] = 0.0;
+  }
+  for (int b = 0; b < 2; ++b)
+    HIPC(c, hipMemcpyAsync(c->d_vu_st[b], st.data(), st.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int omega_vu_update(omega_ctx* c, const void* x, int32_t f64, int64_t n_updates, int32_t chunk, int64_t update_stride,
+                    int64_t channel_stride, const double* dt, double* out, int mem) {
+  if (!c || !out || !dt) return OMEGA_EINVAL;
+  if (!x || n_updates < 0 || chunk < 1) return fail(c, OMEGA_EINVAL, "vu update: bad input layout");
+  if (n_updates == 0) return 0;
+  HIPC(c, hipSetDevice(c->device));
+  const int C = c->cfg.n_channels;
+  const int64_t Wv = (int64_t)(0.3 * c->cfg.sample_rate);  // vu_meters.py:28-30
+  if (!c->d_vu_st[0]) {
+    for (int b = 0; b < 2; ++b) {
+      int e = dalloc(c, &c->d_vu_hist[b], (size_t)C * Wv);
+      if (!e) e = dalloc(c, &c->d_vu_st[b], (size_t)C * 3);
+      if (e) return e;
+    }
+    if (int e = omega_vu_reset(c)) return e;
+  }
+  if (n_updates * C > c->vu_ms_cap) {
+    if (int e = dalloc(c, &c->d_vu_ms, (size_t)n_updates * C)) return e;
+    c->vu_ms_cap = n_updates * C;
+  }
+  std::vector<HostOut> outs;
+  const void* dx = x;
+  const double* ddt = dt;
+  double* dout = out;
+  if (mem == OMEGA_MEM_HOST) {
+    const size_t el = f64 ? 8 : 4;
+    const size_t span = (size_t)((n_updates - 1) * update_stride + (C - 1) * channel_stride + chunk);
+    int e = stage_in(c, 0, x, span * el, &dx);
+    if (!e) e = stage_in(c, 1, dt, (size_t)n_updates * sizeof(double), reinterpret_cast<const void**>(&ddt));
+    if (!e) e = stage_out(c, 2, out, (size_t)n_updates * C * 3, outs, &dout);
+    if (e) return e;
+  }
+  VuParams p{};
+  p.x = dx;
+  p.f64 = f64 ? 1 : 0;
+  p.n = n_updates;
+  p.chunk = chunk;
+  p.frame_stride = update_stride;
+  p.channel_stride = channel_stride;
+  p.C = C;
+  p.dt = ddt;
+  const int a = c->vu_cur, b = a ^ 1;
+  p.hist_in = c->d_vu_hist[a];
+  p.hist_out = c->d_vu_hist[b];
+  p.hist_n = std::min(c->vu_total, Wv);
+  p.Wv = Wv;
+  p.ms = c->d_vu_ms;
+  p.st_in = c->d_vu_st[a];
+  p.st_out = c->d_vu_st[b];
+  p.out = dout;
+  HIPC(c, launch_vu(p, c->stream));
+  c->vu_cur = b;
+  c->vu_total += n_updates * chunk;
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+// Savitzky-Golay (21, 3) weights of scipy.signal.savgol_filter's 'interp' mode: the least-squares
+// cubic through the 21 samples of a window evaluated at window position p (p = 10: the interior
+// convolution; p < 10 / p > 10: the first / last 10 outputs of a frame), in centred, scaled
+// coordinates u = (t - 10) / 10 so that the 4 x 4 normal equations stay well conditioned.
+static void savgol_21_3(double W[21][21]) {
+  double A[21][4], G[4][4] = {};
+  for (int t = 0; t < 21; ++t)
+    for (int j = 0; j < 4; ++j) A[t][j] = std::pow((t - 10) / 10.0, j);
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j)
+      for (int t = 0; t < 21; ++t) G[i][j] += A[t][i] * A[t][j];
+  double Gi[4][4];  // Gauss-Jordan inverse
+  double M[4][8];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 8; ++j) M[i][j] = j < 4 ? G[i][j] : (j - 4 == i ? 1.0 : 0.0);
+  for (int c = 0; c < 4; ++c) {
+    int pv = c;
+    for (int r = c + 1; r < 4; ++r)
+      if (std::fabs(M[r][c]) > std::fabs(M[pv][c])) pv = r;
+    for (int j = 0; j < 8; ++j) std::swap(M[c][j], M[pv][j]);
+    const double d = M[c][c];
+    for (int j = 0; j < 8; ++j) M[c][j] /= d;
+    for (int r = 0; r < 4; ++r)
+      if (r != c) {
+        const double f = M[r][c];
+        for (int j = 0; j < 8; ++j) M[r][j] -= f * M[c][j];
+      }
+  }
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) Gi[i][j] = M[i][j + 4];
+  for (int p = 0; p < 21; ++p) {
+    double v[4], q[4] = {};
+    for (int j = 0; j < 4; ++j) v[j] = std::pow((p - 10) / 10.0, j);
+    for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < 4; ++i) q[j] += v[i] * Gi[i][j];
+    for (int t = 0; t < 21; ++t) {
+      double w = 0.0;
+      for (int j = 0; j < 4; ++j) w += q[j] * A[t][j];
+      W[p][t] = w;
+    }
+  }
+}
+
+int omega_transients(omega_ctx* c, const void* x, int32_t f64, int64_t n_frames, int32_t n, int64_t frame_stride,
+                     double* out, int mem) {
+  if (!c || !out) return OMEGA_EINVAL;
+  if (!x || n_frames < 0 || frame_stride < n) return fail(c, OMEGA_EINVAL, "transients: bad frame layout");
+  if (n < 64 || n > 8192 || (n & (n - 1))) return fail(c, OMEGA_EUNSUP, "transients: frame length %d unsupported", n);
+  if (n_frames == 0) return 0;
+  HIPC(c, hipSetDevice(c->device));
+  if (!c->d_sg) {
+    double W[21][21];
+    savgol_21_3(W);
+    std::vector<double> v(&W[0][0], &W[0][0] + 21 * 21);
+    if (int e = upload(c, &c->d_sg, v)) return e;
+  }
+  auto it = c->tr_tw.find(n);
+  if (it == c->tr_tw.end()) {
+    const int K = n / 2;
+    std::vector<double2> t1(K / 2 > 0 ? K / 2 : 1), t2(K + 1);
+    for (int m = 0; m < K / 2; ++m) t1[m] = make_double2(std::cos(2 * M_PI * m / K), -std::sin(2 * M_PI * m / K));
+    for (int q = 0; q <= K; ++q) t2[q] = make_double2(std::cos(2 * M_PI * q / n), -std::sin(2 * M_PI * q / n));
+    double2 *d1 = nullptr, *d2 = nullptr;
+    int e = upload(c, &d1, t1);
+    if (!e) e = upload(c, &d2, t2);
+    if (e) return e;
+    it = c->tr_tw.emplace(n, std::make_pair(d1, d2)).first;
+  }
+  std::vector<HostOut> outs;
+  const void* dx = x;
+  double* dout = out;
+  if (mem == OMEGA_MEM_HOST) {
+    const size_t el = f64 ? 8 : 4;
+    int e = stage_in(c, 0, x, (size_t)((n_frames - 1) * frame_stride + n) * el, &dx);
+    if (!e) e = stage_out(c, 1, out, (size_t)n_frames * kTransientCols, outs, &dout);
+    if (e) return e;
+  }
+  TransientParams p{};
+  p.x = dx;
+  p.f64 = f64 ? 1 : 0;
+  p.n_frames = n_frames;
+  p.n = n;
+  p.frame_stride = frame_stride;
+  p.tw = it->second.first;
+  p.tw2 = it->second.second;
+  p.sg = c->d_sg;
+  p.fs = c->cfg.sample_rate;
+  p.out = dout;
+  HIPC(c, launch_transients(p, c->stream));
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
 }
 
 int omega_drum_reset(omega_ctx* c) {

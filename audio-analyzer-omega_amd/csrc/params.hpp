@@ -300,4 +300,39 @@ struct RfftParams {
   const float2* tw[kMaxLog2];
 };
 
+// VU meter ballistics (vu.hip; vu_meters.py:55-99) over n consecutive update calls of chunk samples
+// per channel: update u of channel c at x + u * frame_stride + c * channel_stride (float32 or float64)
+struct VuParams {
+  const void* x;
+  int f64;
+  int64_t n;
+  int chunk;
+  int64_t frame_stride, channel_stride;
+  int C;
+  const double* dt;        // [n] seconds since the previous update
+  const double* hist_in;   // [C, Wv] the last hist_n samples before this batch, oldest first
+  double* hist_out;        // [C, Wv]
+  int64_t hist_n;
+  int64_t Wv;              // int(0.3 fs): the deque length
+  double* ms;              // [n, C] scratch: window mean squares
+  const double* st_in;     // [C, 3] display, peak, peak_time
+  double* st_out;
+  double* out;             // [n, C, 3] vu_db (+18 offset applied), display, peak_db
+};
+
+// TransientAnalyzer.analyze_transients (transient.hip; transient.py:19-108), one frame per workgroup
+constexpr int kTransientCols = 6;  // detected, attack_time_ms, punch, envelope_peak, envelope_rms, envelope_mean
+struct TransientParams {
+  const void* x;
+  int f64;
+  int64_t n_frames;
+  int n;                    // frame length (power of two 64..8192)
+  int64_t frame_stride;
+  const double2* tw;        // [n/4] e^{-2 pi i m / (n/2)}
+  const double2* tw2;       // [n/2 + 1] e^{-2 pi i q / n}
+  const double* sg;         // [21, 21] Savitzky-Golay (21, 3) weights by output position in the window
+  double fs;
+  double* out;              // [n_frames, kTransientCols]
+};
+
 }  // namespace omega

@@ -76,6 +76,11 @@ EXPORTS = {
     "omega_synchronize": (C.c_int, [C.c_void_p]),
     "omega_get_stream": (C.c_void_p, [C.c_void_p]),
     "omega_get_config": (C.c_int, [C.c_void_p, C.POINTER(Config), C.POINTER(C.c_int)]),
+    "omega_vu_update": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_int64,
+                                  C.c_void_p, C.c_void_p, C.c_int]),
+    "omega_vu_reset": (C.c_int, [C.c_void_p]),
+    "omega_transients": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_void_p,
+                                   C.c_int]),
     "omega_ingest_config_default": (None, [C.POINTER(IngestConfig)]),
     "omega_ingest_create": (C.c_int, [C.c_void_p, C.POINTER(IngestConfig), C.POINTER(C.c_void_p)]),
     "omega_ingest_push": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),

@@ -244,6 +244,26 @@ int omega_spectra(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t 
                   float* bands_out, double* chroma_out, float* mag_out, int mem);
 
 
+/* VU meter ballistics, VUMetersPanel.update (omega4/panels/vu_meters.py:55-99), for n_updates
+ * consecutive update(audio, dt) calls of every channel (one stream each; the reference duplicates its
+ * mono input into L and R): update u of channel c reads chunk samples at x + u*update_stride +
+ * c*channel_stride (float32, or float64 when f64 != 0 -- the app passes its float64 windowed frame);
+ * dt[n_updates] in seconds. out [n_updates, C, 3] float64: the VU level (dBFS + 18 over the last
+ * int(0.3 fs) samples, -60 + 18 when silent), the damped display value and the peak hold. The sample
+ * history and the needle state carry over between calls; omega_vu_reset starts over. */
+int omega_vu_update(omega_ctx* ctx, const void* x, int32_t f64, int64_t n_updates, int32_t chunk, int64_t update_stride,
+                    int64_t channel_stride, const double* dt, double* out, int mem);
+int omega_vu_reset(omega_ctx* ctx);
+
+/* TransientAnalyzer.analyze_transients (omega4/analyzers/transient.py:19-108) for n_frames frames of
+ * n samples (power of two 64..8192; float32, or float64 when f64 != 0), frame f at x + f*frame_stride,
+ * in float64 like scipy: Hilbert envelope, Savitzky-Golay (21, 3) smoothing, attack points where the
+ * envelope's derivative exceeds twice its standard deviation. out [n_frames, 6] float64:
+ * transients_detected, attack_time (ms), punch_factor, envelope_peak, envelope_rms and the smoothed
+ * envelope's mean (the value the reference appends to its envelope_history). */
+int omega_transients(omega_ctx* ctx, const void* x, int32_t f64, int64_t n_frames, int32_t n, int64_t frame_stride,
+                     double* out, int mem);
+
 /* ---- Sustained-stream ingest ------------------------------------------
  * The capture byte stream of omega4/audio/capture.py:546-600 (parec float32le / s16le, fixed chunks
  * of chunk_size samples, s16 scaled by 1/32768), its per-chunk noise gate (:620-641: RMS, background

@@ -48,6 +48,8 @@ def _import_reference():
     from omega4.analyzers.drum_detection import EnhancedKickDetector, EnhancedSnareDetector
     from omega4.optimization.gpu_accelerated_fft import GPUAcceleratedFFT
     from omega4.audio.capture import AudioCaptureConfig, PipeWireMonitorCapture
+    from omega4.panels.vu_meters import VUMetersPanel
+    from omega4.analyzers.transient import TransientAnalyzer
     return SimpleNamespace(**locals())
 
 
@@ -303,6 +305,80 @@ def gen_capture(R):
     np.savez_compressed(os.path.join(OUT, "capture.npz"), **d)
 
 
+def vu_frames(n=240, m=2048, seed=41):
+    """The app's VU input: Hann-windowed float64 frames (omega4_main.py:1077-1082) of a tone whose level
+    steps down (the display falls, the peak holds 2 s and then decays), then a silent stretch."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(m) / FS
+    lv = np.concatenate([np.full(60, 0.5), np.full(60, 0.05), np.full(90, 0.01), np.zeros(30)])[:n]
+    return np.stack([(a * np.sin(2 * np.pi * 440 * t + 0.1 * k) + a * 0.1 * rng.standard_normal(m)) * np.hanning(m)
+                     for k, a in enumerate(lv)])
+
+
+def gen_vu(R):
+    """VUMetersPanel.update over 240 display frames (float64 windowed input, dt = 1/60) and then 40 float32
+    512-sample chunks with varying dt: the level, display and peak after every call."""
+    d = {"versions": VERSIONS}
+    vp = R.VUMetersPanel(FS)
+    x64 = vu_frames()
+    x32 = (0.3 * np.random.default_rng(42).standard_normal((40, 512))).astype(np.float32)
+    dt32 = np.random.default_rng(43).uniform(0.005, 0.05, 40)
+    rec = []
+    for fr in x64:
+        vp.update(fr, 1 / 60)
+        rec.append((vp.vu_left_db, vp.vu_left_display, vp.vu_left_peak_db, vp.vu_right_db))
+    for fr, dt in zip(x32, dt32):
+        vp.update(fr, float(dt))
+        rec.append((vp.vu_left_db, vp.vu_left_display, vp.vu_left_peak_db, vp.vu_right_db))
+    d["x64"], d["x32"], d["dt32"] = x64, x32, dt32
+    d["out"] = np.array(rec, np.float64)
+    np.savez_compressed(os.path.join(OUT, "vu.npz"), **d)
+
+
+def transient_frames(seed=51):
+    """Drum-like frames: decaying clicks and tone bursts at varying positions and sharpness over a noise
+    floor -- float64 Hann-windowed 2048-sample frames (the app's input, omega4_main.py:1241) and raw
+    float32 1024-sample frames."""
+    rng = np.random.default_rng(seed)
+    out64, out32 = [], []
+    for k in range(24):
+        m = 2048
+        t = np.arange(m) / FS
+        x = 0.01 * rng.standard_normal(m)
+        for _ in range(1 + k % 4):
+            p0 = int(rng.integers(50, m - 200))
+            tau = rng.uniform(0.0005, 0.01)
+            f0 = rng.uniform(50, 3000)
+            env = np.where(t >= t[p0], np.exp(-(t - t[p0]) / tau), 0.0)
+            x += rng.uniform(0.2, 0.9) * env * np.sin(2 * np.pi * f0 * (t - t[p0]))
+        out64.append(x * np.hanning(m))
+    for k in range(12):
+        m = 1024
+        x = (0.02 * rng.standard_normal(m)).astype(np.float32)
+        p0 = int(rng.integers(30, m - 100))
+        x[p0:p0 + 60] += (np.linspace(0.8, 0.0, 60) * rng.choice([-1, 1], 60)).astype(np.float32)
+        out32.append(x)
+    return np.stack(out64), np.stack(out32)
+
+
+def gen_transients(R):
+    """TransientAnalyzer.analyze_transients over one analyzer (its envelope history carries over): the
+    returned dicts for float64 2048-sample and float32 1024-sample frames and a 40-sample frame."""
+    d = {"versions": VERSIONS}
+    ta = R.TransientAnalyzer(FS)
+    x64, x32 = transient_frames()
+    keys = ("transients_detected", "attack_time", "punch_factor", "envelope_peak", "envelope_rms")
+    rec = []
+    for fr in list(x64) + list(x32):
+        r = ta.analyze_transients(fr)
+        rec.append([float(r.get(k, np.nan)) for k in keys])
+    short = ta.analyze_transients(np.ones(40))
+    d["x64"], d["x32"], d["out"] = x64, x32, np.array(rec)
+    d["history"] = np.array(ta.get_envelope_history())
+    d["short"] = np.array([short["transients_detected"], short["attack_time"], short["punch_factor"]])
+    np.savez_compressed(os.path.join(OUT, "transients.npz"), **d)
+
+
 def gen_batched(R):
     d = {"versions": VERSIONS}
     bp = R.BatchedFFTProcessor()
@@ -468,6 +544,6 @@ if __name__ == "__main__":
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture"))]:
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients"))]:
         g(R)
         print("wrote", g.__name__)

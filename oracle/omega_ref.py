@@ -883,3 +883,70 @@ def capture_stream(x: np.ndarray, fs: int = 48000, chunk: int = 512, gain: float
 def s16le_samples(data: bytes) -> np.ndarray:
     """capture.py:571-574 for s16le: int16 -> float32 / 32768.0."""
     return np.frombuffer(data, dtype=np.int16).astype(np.float32) / 32768.0
+
+
+# ----------------------------------------------------------------------------------------------
+# SURVEY.md §8(f) row 2 remainder: VU meter ballistics (omega4/panels/vu_meters.py:55-99)
+# ----------------------------------------------------------------------------------------------
+
+
+class VUState:
+    """VUMetersPanel.update for one channel: the 300 ms sample deque (:28-30, :65-68), RMS (:71-72),
+    dBFS + 18 (:76-81, :104-108), damping 0.94 (:84-85) and the 2 s peak hold with 10 dB/s decay
+    stopping at -20 (:88-102)."""
+
+    def __init__(self, fs: float = 48000):
+        self.buf = deque(maxlen=int(300e-3 * fs))
+        self.db, self.display, self.peak, self.peak_time = -60.0, -60.0, -60.0, 0.0
+
+    def update(self, x: np.ndarray, dt: float):
+        if x is None or len(x) == 0:
+            return
+        self.buf.extend(x)  # (the reference appends sample by sample)
+        rms = np.sqrt(np.mean(np.array(self.buf) ** 2))
+        dbfs = 20.0 * np.log10(rms) if rms > 0 else -60.0
+        self.db = dbfs + 18.0
+        self.display += (self.db - self.display) * (1.0 - 0.94)
+        if self.display > self.peak:
+            self.peak, self.peak_time = self.display, 0.0
+        else:
+            self.peak_time += dt
+            if self.peak_time > 2.0:
+                self.peak = max(self.peak - 10.0 * dt, -20.0)
+        return self.db, self.display, self.peak
+
+
+# ----------------------------------------------------------------------------------------------
+# SURVEY.md §8(f) row 4: TransientAnalyzer.analyze_transients (omega4/analyzers/transient.py:19-108)
+# ----------------------------------------------------------------------------------------------
+
+
+class TransientState:
+    """analyze_transients with the envelope history (transient.py:17, :33): scipy.signal.hilbert and
+    savgol_filter (scipy 1.15.3 here), np.diff / np.std threshold, attack time and punch factor."""
+
+    def __init__(self, fs: float = 48000):
+        self.fs = fs
+        self.envelope_history = deque(maxlen=int(0.5 * 60))
+
+    def analyze(self, x: np.ndarray) -> Dict:
+        from scipy import signal as ss
+        if len(x) < 64:
+            return {"transients_detected": 0, "attack_time": 0.0, "punch_factor": 0.0}
+        env = np.abs(ss.hilbert(x))
+        es = ss.savgol_filter(env, min(21, len(env) // 2 * 2 + 1), 3)
+        self.envelope_history.append(np.mean(es))
+        d = np.diff(es)
+        pts = np.where(d > np.std(d) * 2.0)[0]
+        times, punch = [], []
+        for i in pts:
+            if 10 < i < len(es) - 10:
+                s0, pk = max(0, i - 10), es[i]
+                ten = next((j for j in range(s0, i) if es[j] >= pk * 0.1), s0)
+                ninety = next((j for j in range(ten, min(len(es), i + 10)) if es[j] >= pk * 0.9), i)
+                times.append((ninety - ten) / self.fs * 1000)
+            if 5 < i < len(es) - 5:
+                punch.append(max(0.0, np.mean(es[i:i + 5]) - np.mean(es[i - 5:i])))
+        return {"transients_detected": len(pts), "attack_time": np.mean(times) if times else 0.0,
+                "punch_factor": np.mean(punch) if punch else 0.0, "envelope_peak": np.max(es),
+                "envelope_rms": np.sqrt(np.mean(es ** 2))}

@@ -9,6 +9,7 @@ constexpr int ITERS = 4096;
 template <int OP>
 __global__ __launch_bounds__(1024) void k(float* out, float s) {
   float a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  float c0 = a0 + 8, c1 = a0 + 9, c2 = a0 + 10, c3 = a0 + 11, c4 = a0 + 12, c5 = a0 + 13, c6 = a0 + 14, c7 = a0 + 15;
   float b0 = s, b1 = s * 2;
   for (int i = 0; i < ITERS; ++i) {
     if constexpr (OP == 0) {
@@ -24,6 +25,14 @@ __global__ __launch_bounds__(1024) void k(float* out, float s) {
           "v_pk_fma_f32 %0, %0, %4, %4\n v_pk_fma_f32 %1, %1, %4, %4\n v_pk_fma_f32 %2, %2, %4, %4\n v_pk_fma_f32 %3, %3, %4, %4\n"
           : "+v"(*(double*)&a0), "+v"(*(double*)&a2), "+v"(*(double*)&a4), "+v"(*(double*)&a6)
           : "v"(*(double*)&b0));
+    } else if constexpr (OP == 4) {
+      // packed, 8 independent register pairs
+      asm volatile(
+          "v_pk_fma_f32 %0, %0, %8, %8\n v_pk_fma_f32 %1, %1, %8, %8\n v_pk_fma_f32 %2, %2, %8, %8\n v_pk_fma_f32 %3, %3, %8, %8\n"
+          "v_pk_fma_f32 %4, %4, %8, %8\n v_pk_fma_f32 %5, %5, %8, %8\n v_pk_fma_f32 %6, %6, %8, %8\n v_pk_fma_f32 %7, %7, %8, %8\n"
+          : "+v"(*(double*)&a0), "+v"(*(double*)&a2), "+v"(*(double*)&a4), "+v"(*(double*)&a6),
+            "+v"(*(double*)&c0), "+v"(*(double*)&c2), "+v"(*(double*)&c4), "+v"(*(double*)&c6)
+          : "v"(*(double*)&b0));
     } else if constexpr (OP == 2) {
       asm volatile(
           "v_add_f32 %0, %0, %8\n v_add_f32 %1, %1, %8\n v_add_f32 %2, %2, %8\n v_add_f32 %3, %3, %8\n"
@@ -38,7 +47,7 @@ __global__ __launch_bounds__(1024) void k(float* out, float s) {
           : "v"(*(double*)&b0));
     }
   }
-  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7;
 }
 
 template <int OP>
@@ -71,6 +80,7 @@ int main() {
     run<1>("v_pk_fma_f32", thr, d);
     run<2>("v_add_f32", thr, d);
     run<3>("v_pk_add_f32", thr, d);
+    run<4>("v_pk_fma_f32 x8", thr, d);
   }
   return 0;
 }
