@@ -229,6 +229,7 @@ struct omega_ctx {
     float* w1 = nullptr;
     unsigned short* perm = nullptr;
     int* goff = nullptr;
+    float4* rec = nullptr;
   } ctab;
   int n_cu = 0;
   // drum-feature stream state (omega_drum_features), double-buffered, for drum_bins bins per frame
@@ -239,6 +240,8 @@ struct omega_ctx {
   long long* d_dpos[2] = {};
   float* d_dflux = nullptr;
   PostParams post{};  // omega_post_configure's tables (post.n_bins = 0: not configured)
+  float* d_post_raw = nullptr;  // post-processing band scratch (pre-EMA values)
+  int64_t post_raw_cap = 0;
   // VU meter state (omega_vu_update), double-buffered: sample history, display / peak / hold time
   double* d_vu_hist[2] = {};
   double* d_vu_st[2] = {};
@@ -1366,6 +1369,11 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   p.spec_out = spectrum_out;
   p.band_out = bands_out;
   p.content_out = content_out;
+  if (c->post.nb && n_frames * c->post.nb > c->post_raw_cap) {
+    if (int e = dalloc(c, &c->d_post_raw, (size_t)n_frames * c->post.nb)) return e;
+    c->post_raw_cap = n_frames * c->post.nb;
+  }
+  p.band_raw = c->d_post_raw;
   HIPC(c, launch_post(p, c->stream));
   return 0;
 }
@@ -1392,7 +1400,8 @@ void omega_destroy(omega_ctx* c) {
   if (c->fork[0]) (void)hipStreamSynchronize(c->fork[0]);
   for (void* p : c->allocs) (void)hipFree(p);
   for (auto& kv : c->chroma_mats) (void)hipFree(kv.second.first);
-  for (void* q : {(void*)c->ctab.w4, (void*)c->ctab.w1, (void*)c->ctab.perm, (void*)c->ctab.goff})
+  for (void* q : {(void*)c->ctab.w4, (void*)c->ctab.w1, (void*)c->ctab.perm, (void*)c->ctab.goff,
+                  (void*)c->ctab.rec})
     if (q) (void)hipFree(q);
   for (DevBuf& b : c->stage)
     if (b.p) (void)hipFree(b.p);
@@ -1922,9 +1931,21 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
     }
     goff[12] = (int)perm.size();
     if (perm.empty()) perm.push_back(0);
-    for (void* q : {(void*)c->ctab.w4, (void*)c->ctab.w1, (void*)c->ctab.perm, (void*)c->ctab.goff})
+    std::vector<float4> rec(2 * perm.size());
+    for (size_t j = 0; j < perm.size(); ++j) {
+      const int i = perm[j];
+      rec[2 * j] = w4[i];
+      const int bin = lo + i;
+      float binf;
+      std::memcpy(&binf, &bin, sizeof binf);  // the bin index's bits in the record's second lane
+      rec[2 * j + 1] = make_float4(w1[i], binf, 0.f, 0.f);
+    }
+    for (void* q : {(void*)c->ctab.w4, (void*)c->ctab.w1, (void*)c->ctab.perm, (void*)c->ctab.goff,
+                    (void*)c->ctab.rec})
       if (q) (void)hipFree(q);
     c->ctab = omega_ctx::ChromaTab{};
+    HIPC(c, hipMalloc(&c->ctab.rec, rec.size() * sizeof(float4)));
+    HIPC(c, hipMemcpy(c->ctab.rec, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice));
     HIPC(c, hipMalloc(&c->ctab.w4, w4.size() * sizeof(float4)));
     HIPC(c, hipMalloc(&c->ctab.w1, w1.size() * sizeof(float)));
     HIPC(c, hipMalloc(&c->ctab.perm, perm.size() * sizeof(unsigned short)));
@@ -1975,6 +1996,7 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
   p.cw1 = c->ctab.w1;
   p.cperm = c->ctab.perm;
   p.cgoff = c->ctab.goff;
+  p.crec = c->ctab.rec;
   p.chroma_out = dcr;
   for (int l = 0; l < kMaxLog2; ++l) p.tw[l] = c->d_tw[l];
   const int grid = (int)std::min<int64_t>(n, 2 * (int64_t)c->n_cu);

@@ -29,10 +29,10 @@ __global__ __launch_bounds__(kFrameThreads) void frame_kernel(SpectralParams sp,
   if (kp.lufs_out || kp.weighted_out) {
     // scratch: pwl / sh / edge / double partials at the start of bufA, f parked in bufB
     char* a = reinterpret_cast<char*>(bufA);
-    auto* pwl = reinterpret_cast<float4(*)[64]>(a);                       // 2 KiB
-    auto* sh = reinterpret_cast<float*>(a + 2 * 64 * sizeof(float4));     // 4 * NW floats
+    auto* pwl = reinterpret_cast<float4(*)[kPwl]>(a);                     // 3 KiB
+    auto* sh = reinterpret_cast<float*>(a + 2 * kPwl * sizeof(float4));   // 4 * NW floats
     auto* edge = sh + 4 * NW;                                              // 20 floats
-    auto* redd = reinterpret_cast<double*>(a + 4096);                     // NW doubles
+    auto* redd = reinterpret_cast<double*>(a + 2 * kPwl * sizeof(float4) + 2048);  // NW doubles
     kweight_body<M, NTH>(kp, cf, tid, pwl, reinterpret_cast<float*>(bufB), sh, edge, redd);
     __syncthreads();
   }

@@ -95,7 +95,10 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
     static_for<0, S>([&](auto j) {
       // sub-chunk j in processing order covers samples (REV: from the end) j*LS .. j*LS + LS - 1
       constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
-      bq_state(t, u[n], e0[j], e1[j]);
+      if constexpr (kKwCorr)
+        u[n] = bq_step(t, u[n], e0[j], e1[j]);  // zero-state outputs, corrected in step 5
+      else
+        bq_state(t, u[n], e0[j], e1[j]);
     });
   });
   float s0 = e0[0], s1 = e1[0];
@@ -179,11 +182,33 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
   // through an opaque copy first (OPQ, the batch kernel): otherwise the compiler keeps step 1's B1 * u
   // products live across the scan for reuse here -- L more live registers, spilled there; the
   // standalone kernel runs faster without the copy.)
-  if constexpr (OPQ) {
+  if constexpr (OPQ && !kKwCorr) {
 #pragma unroll
     for (int i = 0; i < L; ++i) asm volatile("" : "+v"(u[i]));
   }
-  {
+  if constexpr (kKwCorr) {
+    // y = y_zero + (A^i s_in)[0]: the zero-state outputs plus the first row of A^i (h0, h1) times the
+    // sub-chunk's true incoming state -- independent multiply-adds instead of a second serial pass
+    float r0[S], r1[S];
+    r0[0] = i0;
+    r1[0] = i1;
+    static_for<1, S>([&](auto j) {
+      float q0, q1;
+      mv4(t.ps, r0[j - 1], r1[j - 1], q0, q1);
+      r0[j] = q0 + e0[j - 1];
+      r1[j] = q1 + e1[j - 1];
+    });
+    static_for<0, LS>([&](auto i) {
+      // (groups of 8 rows: the LDS reads are not all hoisted into registers at once)
+      if constexpr (i % 8 == 0) asm volatile("" ::: "memory");
+      const float4 hg = pwl[64 + i];  // (h0, h1) of A^i, LDS broadcast
+      const float g0 = hg.x, g1 = hg.y;
+      static_for<0, S>([&](auto j) {
+        constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
+        u[n] = fmaf(g1, r1[j], fmaf(g0, r0[j], u[n]));
+      });
+    });
+  } else {
     float r0[S], r1[S];
     r0[0] = i0;
     r1[0] = i1;
@@ -265,22 +290,23 @@ __device__ __forceinline__ void kw_count_in(const KWeightParams& p, int tid) {
 }
 
 // K-weighting of channel-frame cf by a workgroup of NTH threads (all of them), chunk L = M / NTH
-// (the host tables must be built for that L). LDS from the caller: pwl[2][64] scan powers, fbuf[M]
+// (the host tables must be built for that L). LDS from the caller: pwl[2][kPwl] scan tables, fbuf[M]
 // parking for f (element-major), sh[4 * NW], edge[20], red[NW].
 template <int M, int NTH, bool PUB = false, bool OPQ = false>
-__device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf, int tid, float4 (*pwl)[64], float* fbuf,
+__device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf, int tid, float4 (*pwl)[kPwl], float* fbuf,
                                              float* sh, float* edge, double* red) {
   constexpr int L = M / NTH;
-  static_assert(L <= 64 && L * NTH == M, "chunk length");
+  static_assert(L <= 32 && L * NTH == M, "chunk length (the A^i rows of the LDS table cover i < 32)");
   const int64_t f = cf / p.C, c = cf % p.C;
   const float* __restrict__ x = p.x + f * p.frame_stride + c * p.chan_stride;
   const BiquadTab& hp = *p.hp;
   const BiquadTab& shelf = *p.shelf;  // (the scan matrices of both, lane-indexed, to LDS)
   OMEGA_STAMP(0);
-  for (int i = tid; i < 128; i += NTH) {
-    const BiquadTab& t = i < 64 ? hp : shelf;
-    const int l = i & 63;
-    pwl[i >> 6][l] = make_float4(t.pw[l][0], t.pw[l][1], t.pw[l][2], t.pw[l][3]);
+  for (int i = tid; i < 2 * kPwl; i += NTH) {
+    const BiquadTab& t = i < kPwl ? hp : shelf;
+    const int l = i % kPwl;
+    pwl[i / kPwl][l] = l < 64 ? make_float4(t.pw[l][0], t.pw[l][1], t.pw[l][2], t.pw[l][3])
+                              : make_float4(t.h0[l - 64], t.h1[l - 64], 0.f, 0.f);
   }
   float u[L];
   if constexpr (L % 4 == 0) {

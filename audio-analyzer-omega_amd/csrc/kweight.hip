@@ -42,7 +42,7 @@ template <int M, bool PUB = false, int NTH = kw_threads(M)>
 __global__ __launch_bounds__(NTH, kw_waves_per_eu(NTH)) void kweight_kernel(KWeightParams p) {
   constexpr int NW = NTH / 64;
   static_assert(M / NTH == kw_chunk(M), "chunk length must match the host tables");
-  __shared__ float4 pwl[2][64];  // P^(l+1) of both filters, for the lane-indexed step of the scan
+  __shared__ float4 pwl[2][kPwl];  // scan powers and A^i rows of both filters (kw.hpp)
   __shared__ float fbuf[M];      // f, element-major (fbuf[i * NTH + t]): conflict-free, own data only
   __shared__ float sh[4 * NW];
   __shared__ float edge[20];

@@ -65,6 +65,17 @@ struct BiquadTab {
 #define OMEGA_KW_SUB 1
 #endif
 constexpr int kKwSub = OMEGA_KW_SUB;
+// lfilter_pass: zero-state outputs + first-row-of-A^i correction (1) or a zero-state state pass and a
+// second serial pass from the true incoming state (0, default). The correction form has 7 instead of
+// 9 VALU ops per sample and one serial chain instead of two, but its live ranges cost ~28 VGPRs: the
+// batch kernel spilled (private segment 8 -> 136-444 B) and took 126 vs 77 us (MI355X, round 2).
+#ifndef OMEGA_KW_CORR
+#define OMEGA_KW_CORR 0
+#endif
+constexpr bool kKwCorr = OMEGA_KW_CORR != 0;
+// K-weighting LDS table per filter (float4 entries): [0, 64) the scan powers P^(l+1), [64, 96) the
+// first row of A^i, i < 32, as (h0, h1, -, -) -- read at the correction, not held in registers
+constexpr int kPwl = 96;
 
 // K-weighting workgroup: up to 32 samples per thread (M/32 threads, 64..512), the chunk length L of
 // the scan tables (make_biquad_tab) follows from it.
@@ -233,6 +244,9 @@ struct SpectraParams {
   const float* cw1;
   const unsigned short* cperm;
   const int* cgoff;        // [13]
+  // the same weights permuted into group order as 32-byte records {w0, w1, w2, w3 | w4, bin, -, -}
+  // (the register-FFT kernel reads record j directly: no dependent permutation load)
+  const float4* crec;      // [2 * cgoff[12]]
   double* chroma_out;      // [n, 12] or nullptr (smoothed, normalised; before the temporal blend)
   const float2* tw[kMaxLog2];
 };
@@ -266,6 +280,7 @@ struct PostParams {
   float bass_boost;
   float* spec_out;             // [n, T]
   float* band_out;             // [n, nb]
+  float* band_raw;             // [n, nb] scratch: the clamped band values before the EMA
   int* content_out;            // [n]
   float* prev;                 // [nb] EMA state
   int* has_prev;

@@ -17,7 +17,7 @@
 // percentile's lerp into an FMA (1 ulp off the reference value on the last golden frame, then every
 // bin of that frame).
 //   post_frame_kernel: one 256-thread workgroup per frame (independent frames).
-//   post_ema_kernel: one workgroup, one thread per band, the frames in order (the EMA recurrence).
+//   post_ema_kernel: one thread per band, the frames in order (the EMA recurrence), loads in blocks.
 #include "fft.hpp"
 #include "numpy_emul.hpp"
 #include "params.hpp"
@@ -144,37 +144,72 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
       v = s[lo];
     }
     if (v > 0.f) v = fminf(__fsqrt_rn(v), 1.0f);
-    p.band_out[f * p.nb + b] = v;
+    p.band_raw[f * p.nb + b] = v;
   }
   if (t == 0 && p.content_out) p.content_out[f] = content;
 }
 
-// band_out holds the clamped band values of the n frames; the EMA runs over them in frame order
-__global__ __launch_bounds__(kPostMaxBands) void post_ema_kernel(PostParams p) {
-  const int b = threadIdx.x;
+// band_raw holds the clamped band values of the n frames; the EMA runs over them in frame order into
+// band_out.
+// One thread per (band, chunk of kEmaChunk frames). The first chunk continues the stream's state; a
+// later chunk starts kEmaWarm frames early from that frame's value (as at a stream start) and runs
+// the same float32 recurrence up to its own frames: the warm-up's starting point contributes
+// sf^kEmaWarm <= 0.85^256 ~ 1e-18 of the value, far below float32 resolution, so the chunk joins the
+// sequential sequence bit for bit (a residual 1-ulp difference must survive ~200 roundings in a row;
+// tests/test_gpu_parity.py checks a 700-frame call against sequential calls bitwise).
+// Loads go in blocks of kEmaBlock frames (independent loads in flight; the recurrence is the only
+// dependence).
+constexpr int kEmaBlock = 32;
+constexpr int kEmaChunk = 128;
+constexpr int kEmaWarm = 256;
+__global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.y * kEmaChunk;
+  if (b >= p.nb || c0 >= p.n) return;
   const bool had = *p.has_prev != 0;
-  __syncthreads();
-  if (b < p.nb) {
-    const float sf = p.sf[b], sf1 = p.sf[p.nb + b];  // float32(f), float32(1 - f)
-    float prev = had ? p.prev[b] : 0.f;
-    bool have = had;
-    for (int64_t f = 0; f < p.n; ++f) {
-      float v = p.band_out[f * p.nb + b];
-      if ((p.flags & 8) && have) v = prev * sf + v * sf1;
-      p.band_out[f * p.nb + b] = v;
-      prev = v;
-      have = true;
+  const float sf = p.sf[b], sf1 = p.sf[p.nb + b];  // float32(f), float32(1 - f)
+  const bool smooth = (p.flags & 8) != 0;
+  const int64_t c1 = c0 + kEmaChunk < p.n ? c0 + kEmaChunk : p.n;
+  const int64_t s0 = c0 == 0 ? 0 : (c0 > kEmaWarm ? c0 - kEmaWarm : 0);
+  const bool exact_start = c0 == 0 || s0 == 0;
+  float prev = (exact_start && had) ? p.prev[b] : 0.f;
+  bool have = exact_start ? had : false;
+  const float* col = p.band_raw + b;
+  float* dst = p.band_out + b;
+  for (int64_t f0 = s0; f0 < c1; f0 += kEmaBlock) {
+    float v[kEmaBlock];
+    const int nf = c1 - f0 < kEmaBlock ? (int)(c1 - f0) : kEmaBlock;
+#pragma unroll
+    for (int i = 0; i < kEmaBlock; ++i)
+      if (i < nf) v[i] = col[(f0 + i) * p.nb];
+#pragma unroll
+    for (int i = 0; i < kEmaBlock; ++i) {
+      if (i < nf) {
+        if (smooth && have) v[i] = prev * sf + v[i] * sf1;
+        prev = v[i];
+        have = true;
+      }
     }
-    p.prev[b] = prev;
+    // only this chunk's frames are written (the warm-up frames belong to the chunk before)
+    if (f0 + kEmaBlock > c0) {
+#pragma unroll
+      for (int i = 0; i < kEmaBlock; ++i)
+        if (i < nf && f0 + i >= c0) dst[(f0 + i) * p.nb] = v[i];
+    }
   }
-  if (b == 0 && p.n > 0) *p.has_prev = 1;
+  if (c1 == p.n) p.prev[b] = prev;
 }
+
+__global__ void post_flag_kernel(int* has_prev) { *has_prev = 1; }
 
 hipError_t launch_post(const PostParams& p, hipStream_t s) {
   if (p.T < 1 || p.T > kPostMaxBins || p.nb < 0 || p.nb > kPostMaxBands) return hipErrorInvalidValue;
   if (p.n == 0) return hipSuccess;
   hipLaunchKernelGGL(post_frame_kernel, dim3((unsigned)p.n), dim3(kPostThreads), 0, s, p);
-  hipLaunchKernelGGL(post_ema_kernel, dim3(1), dim3(kPostMaxBands), 0, s, p);
+  if (p.nb > 0)
+    hipLaunchKernelGGL(post_ema_kernel, dim3((p.nb + 63) / 64, (unsigned)((p.n + kEmaChunk - 1) / kEmaChunk)), dim3(64), 0,
+                       s, p);
+  hipLaunchKernelGGL(post_flag_kernel, dim3(1), dim3(1), 0, s, p.has_prev);
   return hipGetLastError();
 }
 

@@ -354,18 +354,24 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     const int g = t / kGrp, r = t % kGrp;
     const int j0 = p.cgoff[g], j1 = p.cgoff[g + 1];
-    for (int j = j0 + r; j < j1; j += kGrp) {
-      const int i = p.cperm[j];
-      const int k = p.c_lo + i;
-      const float e = magc[k];  // (suppressed above)
-      const float4 cw = p.cw4[i];
-      const double ed = (double)e;
-      acc[0] = fma(ed, (double)cw.x, acc[0]);
-      acc[1] = fma(ed, (double)cw.y, acc[1]);
-      acc[2] = fma(ed, (double)cw.z, acc[2]);
-      acc[3] = fma(ed, (double)cw.w, acc[3]);
-      acc[4] = fma(ed, (double)p.cw1[i], acc[4]);
+    // group-ordered 32-byte records (weights + bin): two records per iteration, all four loads of an
+    // iteration independent (no permutation load in front of the weights)
+    auto acc_rec = [&](const float4 a, const float4 b) {
+      const double ed = (double)magc[__float_as_int(b.y)];  // (suppressed above)
+      acc[0] = fma(ed, (double)a.x, acc[0]);
+      acc[1] = fma(ed, (double)a.y, acc[1]);
+      acc[2] = fma(ed, (double)a.z, acc[2]);
+      acc[3] = fma(ed, (double)a.w, acc[3]);
+      acc[4] = fma(ed, (double)b.x, acc[4]);
+    };
+    int j = j0 + r;
+    for (; j + kGrp < j1; j += 2 * kGrp) {
+      const float4 a0 = p.crec[2 * j], b0 = p.crec[2 * j + 1];
+      const float4 a1 = p.crec[2 * (j + kGrp)], b1 = p.crec[2 * (j + kGrp) + 1];
+      acc_rec(a0, b0);
+      acc_rec(a1, b1);
     }
+    if (j < j1) acc_rec(p.crec[2 * j], p.crec[2 * j + 1]);
 #pragma unroll
     for (int o = 0; o < 5; ++o) part[t * 5 + o] = acc[o];
   }
@@ -433,7 +439,7 @@ __device__ __forceinline__ void batch_multi(const SpectralParams& p, int r, int6
   mrfft_frame<K, G>(p, r, valid ? cf : p.n_cf - 1, valid, tid % G, smem + grp * K);
 }
 
-// K-weighting role (kweight_kernel's LDS, carved: pwl 2 KiB | fbuf 64 KiB | sh 32 floats | edge 20
+// K-weighting role (kweight_kernel's LDS, carved: pwl 3 KiB | fbuf 64 KiB | sh 32 floats | edge 20
 // floats | red 8 doubles). OMEGA_BATCH_KW_NOINLINE: a call with its own register allocation.
 #ifdef OMEGA_BATCH_KW_NOINLINE
 __device__ __attribute__((noinline))
@@ -441,11 +447,13 @@ __device__ __attribute__((noinline))
 __device__ __forceinline__
 #endif
 void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
-  auto* pwl = reinterpret_cast<float4(*)[64]>(smem);
-  float* fbuf = reinterpret_cast<float*>(smem + 2048);
-  float* sh = reinterpret_cast<float*>(smem + 2048 + 65536);
+  constexpr int kP = 2 * kPwl * 16;  // pwl bytes
+  auto* pwl = reinterpret_cast<float4(*)[kPwl]>(smem);
+  float* fbuf = reinterpret_cast<float*>(smem + kP);
+  float* sh = reinterpret_cast<float*>(smem + kP + 65536);
   float* edge = sh + 32;
-  double* red = reinterpret_cast<double*>(smem + 2048 + 65536 + 208);
+  double* red = reinterpret_cast<double*>(smem + kP + 65536 + 208);
+  static_assert(kP + 65536 + 208 + 64 <= lds_bytes<8192>(), "K-weighting role LDS");
   // (one instantiation: the value is always stored write-through; a second copy of the body costs
   // the kernel another set of spill slots)
   kweight_body<16384, kBatchThreads, true, true>(kp, cf, tid, pwl, fbuf, sh, edge, red);

@@ -803,3 +803,20 @@ def test_app_post_random_state_and_device_input():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(torch.cat([p[0] for p in parts]).cpu().numpy(), s)
     np.testing.assert_array_equal(torch.cat([p[1] for p in parts]).cpu().numpy(), b)
+
+
+def test_app_post_ema_chunks_join_the_sequential_recurrence():
+    """700 frames in one call (the band EMA runs as 6 chunks of 128 frames, the later ones warmed up
+    over the 256 frames before them) give bit for bit the bands of 7 sequential calls of 100 frames
+    (each one chunk that continues the carried state), and match the oracle."""
+    from omega_gpu.app_post import SpectrumPostProcessor
+    freqs = load_golden("app_post")["default/freqs"]
+    rng = np.random.default_rng(12)
+    x = (rng.random((700, 512)) * rng.random((700, 1)) ** 2).astype(np.float32)
+    s1, b1, c1 = SpectrumPostProcessor(freqs).process(x)
+    pp = SpectrumPostProcessor(freqs)
+    parts = [pp.process(x[i:i + 100]) for i in range(0, 700, 100)]
+    np.testing.assert_array_equal(b1, np.concatenate([p[1] for p in parts]))
+    np.testing.assert_array_equal(s1, np.concatenate([p[0] for p in parts]))
+    ws, wb, wc = R.app_post_sequence(x, freqs)
+    np.testing.assert_allclose(b1, wb, rtol=POST_BAND_RTOL, atol=POST_BAND_ATOL)
