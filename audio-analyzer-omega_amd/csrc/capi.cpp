@@ -199,6 +199,9 @@ struct omega_ctx {
   std::string err;
   // tables
   float2* d_tw[kMaxLog2] = {};
+  float4* d_rtw1[2] = {};  // register-FFT twiddle tables (build_rf_twiddles), K = 4096 / 8192
+  float4* d_rtw2[2] = {};
+
   float2* d_rot = nullptr;
   float* d_win[kMaxRes] = {};
   float* d_wgt[kMaxRes] = {};
@@ -460,6 +463,34 @@ int tp_scratch(omega_ctx* c, int W, int64_t n_cf, float4** out) {
   return 0;
 }
 
+// Register-FFT inter-pass twiddle tables (regfft.hpp RegFFT::run): for K = 4096 and 8192 points,
+// rtw1[j * NTH + t] = (W^{t (2j+1)}, W^{t (2j+2)}) and rtw2[j * L + u] = (W^{16u (2j+1)}, W^{16u (2j+2)}),
+// W = e^{-2 pi i / K}, j < 8 (float64 angles rounded once to float32).
+int build_rf_twiddles(omega_ctx* c) {
+  for (int i = 0; i < 2; ++i) {
+    const int K = i ? 8192 : 4096, NTH = K / 16, L = K / 256;
+    auto w = [&](long long m) {
+      const double a = -2.0 * M_PI * (double)(m % K) / K;
+      return std::make_pair((float)std::cos(a), (float)std::sin(a));
+    };
+    std::vector<float4> t1((size_t)8 * NTH), t2((size_t)8 * L);
+    for (int j = 0; j < 8; ++j) {
+      for (int t = 0; t < NTH; ++t) {
+        const auto a = w((long long)t * (2 * j + 1)), b = w((long long)t * (2 * j + 2));
+        t1[(size_t)j * NTH + t] = make_float4(a.first, a.second, b.first, b.second);
+      }
+      for (int u = 0; u < L; ++u) {
+        const auto a = w(16LL * u * (2 * j + 1)), b = w(16LL * u * (2 * j + 2));
+        t2[(size_t)j * L + u] = make_float4(a.first, a.second, b.first, b.second);
+      }
+    }
+    int e = upload(c, &c->d_rtw1[i], t1);
+    if (!e) e = upload(c, &c->d_rtw2[i], t2);
+    if (e) return e;
+  }
+  return 0;
+}
+
 int build_spectral_tables(omega_ctx* c) {
   const omega_config& cfg = c->cfg;
   const double fs = cfg.sample_rate;
@@ -624,6 +655,10 @@ SpectralParams spectral_params(omega_ctx* c) {
   p.C = c->cfg.n_channels;
   p.n_res = c->cfg.n_res;
   p.rf_sizes = c->rf_sizes;
+  for (int i = 0; i < 2; ++i) {
+    p.rtw1[i] = c->d_rtw1[i];
+    p.rtw2[i] = c->d_rtw2[i];
+  }
   for (int r = 0; r < p.n_res; ++r) {
     ResParam& q = p.res[r];
     q.n = c->cfg.res[r].fft_size;
@@ -1022,6 +1057,7 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   }
   e = build_twiddles(c);
   if (!e) e = build_spectral_tables(c);
+  if (!e) e = build_rf_twiddles(c);
   if (!e) e = build_meter_state(c);
   *out = c;
   return e;
@@ -1997,6 +2033,8 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
   p.cperm = c->ctab.perm;
   p.cgoff = c->ctab.goff;
   p.crec = c->ctab.rec;
+  p.rtw1 = c->d_rtw1[0];
+  p.rtw2 = c->d_rtw2[0];
   p.chroma_out = dcr;
   for (int l = 0; l < kMaxLog2; ++l) p.tw[l] = c->d_tw[l];
   const int grid = (int)std::min<int64_t>(n, 2 * (int64_t)c->n_cu);

@@ -47,6 +47,10 @@ struct SpectralParams {
   // oversampling (the reference's default), 0x4 = 2x (n + 1/2 only), 0 = 1x (the samples)
   int tp_phases;
   const float2* tw[kMaxLog2];  // tw[l][m] = exp(-2 pi i m / 2^l)
+  // register-FFT inter-pass twiddle tables per size (index 0: K = 4096, 1: K = 8192; null: power
+  // chains): rtw1[j * NTH + t] = (W_K^{t (2j+1)}, W_K^{t (2j+2)}), rtw2[j * L + u] the same for 16 u
+  const float4* rtw1[2];
+  const float4* rtw2[2];
   int rf_sizes;  // host-side launch choice: bit log2(N) set = resolution size N runs on the register-FFT kernel
 };
 
@@ -76,6 +80,14 @@ constexpr bool kKwCorr = OMEGA_KW_CORR != 0;
 // K-weighting LDS table per filter (float4 entries): [0, 64) the scan powers P^(l+1), [64, 96) the
 // first row of A^i, i < 32, as (h0, h1, -, -) -- read at the correction, not held in registers
 constexpr int kPwl = 96;
+// register-FFT inter-pass twiddles from tables (1) or power chains (0, default). The tables cut the
+// FFT roles' VALU count (true peak 2584 -> 2396 static instructions) but ran slower on MI355X (round 2:
+// true peak 37.5 vs 36.4 us, batch 79.5 vs 78.1, cfg3 67.1 vs 65.6): these kernels are bound by LDS
+// exchanges and barriers, not VALU issue, and the table loads add latency.
+#ifndef OMEGA_RF_TWTAB
+#define OMEGA_RF_TWTAB 0
+#endif
+constexpr bool kRfTab = OMEGA_RF_TWTAB != 0;
 
 // K-weighting workgroup: up to 32 samples per thread (M/32 threads, 64..512), the chunk length L of
 // the scan tables (make_biquad_tab) follows from it.
@@ -247,6 +259,8 @@ struct SpectraParams {
   // the same weights permuted into group order as 32-byte records {w0, w1, w2, w3 | w4, bin, -, -}
   // (the register-FFT kernel reads record j directly: no dependent permutation load)
   const float4* crec;      // [2 * cgoff[12]]
+  const float4* rtw1;      // register-FFT twiddle tables for K = 4096 (SpectralParams::rtw1)
+  const float4* rtw2;
   double* chroma_out;      // [n, 12] or nullptr (smoothed, normalised; before the temporal blend)
   const float2* tw[kMaxLog2];
 };

@@ -90,15 +90,37 @@ struct RegFFT {
     static_for<0, 16>([&](auto m) { v[m] = o[m]; });
   }
 
+  // v[k] *= T[k], k = 1..15, from a twiddle table: tab[j * stride] = (T[2j + 1], T[2j + 2]), j < 8
+  static __device__ __forceinline__ void twiddle_tab(float2 (&v)[16], const float4 (&q)[8]) {
+    static_for<0, 8>([&](auto j) {
+      v[2 * j + 1] = cmul(v[2 * j + 1], make_float2(q[j].x, q[j].y));
+      if constexpr (2 * j + 2 < 16) v[2 * j + 2] = cmul(v[2 * j + 2], make_float2(q[j].z, q[j].w));
+    });
+  }
+  static __device__ __forceinline__ void load_tab(float4 (&q)[8], const float4* __restrict__ tab, int stride) {
+    static_for<0, 8>([&](auto j) { q[j] = tab[j * stride]; });
+  }
+
   // Forward FFT. In: v[r] = x[t + NTH r]. Out: v[m] = X[out_index(t, m)]. w1 = W_K^t and
   // w2 = W_K^{16 (t mod L)} (the thread's twiddle bases, loaded once per kernel). SYNC: `buf` may
   // still be read by other threads on entry -- a barrier precedes the first exchange write (after
-  // pass 1's arithmetic, so the butterflies overlap the stragglers' reads).
-  template <bool SYNC = false>
-  static __device__ __forceinline__ void run(float2 (&v)[16], float2* buf, int t, float2 w1, float2 w2) {
+  // pass 1's arithmetic, so the butterflies overlap the stragglers' reads). tw1 / tw2 (optional):
+  // the inter-pass twiddles as tables (RfTw), loaded ahead of each pass's DFT instead of formed by
+  // power chains (14 complex multiplications per pass).
+  template <bool SYNC = false, bool TAB = false>
+  static __device__ __forceinline__ void run(float2 (&v)[16], float2* buf, int t, float2 w1, float2 w2,
+                                             const float4* __restrict__ tw1 = nullptr,
+                                             const float4* __restrict__ tw2 = nullptr) {
     // pass 1
-    dft16(v);
-    twiddle(v, w1);
+    if constexpr (TAB) {
+      float4 q[8];
+      load_tab(q, tw1 + t, NTH);
+      dft16(v);
+      twiddle_tab(v, q);
+    } else {
+      dft16(v);
+      twiddle(v, w1);
+    }
     if constexpr (SYNC) __syncthreads();
     {
       float2* b = buf + t;
@@ -110,8 +132,15 @@ struct RegFFT {
       const int u = t % L, k1 = t / L;
       const float2* b = buf + P1 * k1 + u;
       static_for<0, 16>([&](auto r) { v[r] = b[L * r]; });
-      dft16(v);
-      twiddle(v, w2);
+      if constexpr (TAB) {
+        float4 q[8];
+        load_tab(q, tw2 + u, L);
+        dft16(v);
+        twiddle_tab(v, q);
+      } else {
+        dft16(v);
+        twiddle(v, w2);
+      }
       __syncthreads();  // every exchange-1 read is done
       float2* bw = buf + P2R * k1 + u;
       static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });

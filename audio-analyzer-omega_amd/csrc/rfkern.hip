@@ -43,18 +43,27 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
   const float2* __restrict__ twM = p.tw[ilog2(M)];
   float2 v[16];
   float mx = 0.f;  // p = 0 phase: the samples themselves
+  OMEGA_STAMP(0);
+  // the thread's twiddle bases first: their (L2-resident) loads return while the frame streams in,
+  // instead of behind it (vmcnt waits in issue order) at the first pass's twiddle multiply
+  const float2 w1 = twK[t], w2 = twK[16 * (t % FFT::L)];
+  const float2 wm = twM[t];     // W_M^t
+  const float2 rho = p.rot[t];  // e^{2 pi i t / 4M}
+  asm volatile("" ::: "memory");  // (keeps the scheduler from sinking them behind the frame loads)
   static_for<0, 16>([&](auto r) {
     v[r] = x2[t + NTH * r];
     mx = fmaxf(mx, fmaxf(fabsf(v[r].x), fabsf(v[r].y)));
   });
-  const float2 w1 = twK[t], w2 = twK[16 * (t % FFT::L)];
-  const float2 wm = twM[t];     // W_M^t
-  const float2 rho = p.rot[t];  // e^{2 pi i t / 4M}
-  FFT::run(v, buf, t, w1, w2);
+  OMEGA_STAMP(1);
+  const float4* __restrict__ rt1 = p.rtw1[K == 8192];
+  const float4* __restrict__ rt2 = p.rtw2[K == 8192];
+  FFT::template run<false, kRfTab>(v, buf, t, w1, w2, rt1, rt2);
+  OMEGA_STAMP(2);
   // natural-order spectrum -> X_k on k in S_t
   __syncthreads();
   FFT::store_spectrum(v, buf, t);
   __syncthreads();
+  OMEGA_STAMP(3);
   float xn = 0.f;  // X_K (thread 0)
   {
     const float2* bo = buf + FFT::s3(t);
@@ -81,6 +90,7 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
   // i e^{2 pi i t / M} / 2: alpha_k = (1/2, 0) + (that) e^{2 pi i r / 32}
   const float2 hz = make_float2(0.5f * wm.y, 0.5f * wm.x);
   float fmx = 0.f;
+  OMEGA_STAMP(4);
 #pragma unroll 1
   for (int P = 1; P <= 3; ++P) {
     // opaque per-iteration copies: keep the inlined FFT's address arithmetic and twiddle powers
@@ -94,12 +104,14 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
       y[r] = cmul(y[r], rk);
     });
     if (!((p.tp_phases >> P) & 1)) continue;  // phase not requested (oversampling 2 or 1)
+    OMEGA_STAMP(1 + 4 * P);
     __syncthreads();  // the previous transform's last exchange reads are done
     {
       float2* bo = buf + FFT::s3(tl);
       static_for<0, 16>([&](auto r) { bo[FFT::o3(r)] = y[r]; });
     }
     __syncthreads();
+    OMEGA_STAMP(2 + 4 * P);
     const float cp = P == 1 ? 7.071067812e-01f : (P == 2 ? 0.f : -7.071067812e-01f);
     const float2* bm = buf + FFT::s3m(tl);
     static_for<0, 16>([&](auto r) {
@@ -115,8 +127,10 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
       const float2 d = csub(y[r], yp);
       v[r] = cconj(cadd(yp, cmul(al, d)));
     });
-    FFT::template run<true>(v, buf, tl, w1l, w2l);
+    OMEGA_STAMP(3 + 4 * P);
+    FFT::template run<true, kRfTab>(v, buf, tl, w1l, w2l, rt1, rt2);
     static_for<0, 16>([&](auto m) { fmx = fmaxf(fmx, fmaxf(fabsf(v[m].x), fabsf(v[m].y))); });
+    OMEGA_STAMP(4 + 4 * P);
   }
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, t);
   if (t == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
@@ -125,6 +139,13 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
 template <int K>
 __global__ __launch_bounds__(K / 16, 4) void truepeak_rf_kernel(SpectralParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef OMEGA_TP_STAGGER
+  // development experiment: the second half of the grid (the workgroups that share a CU with the
+  // first half's) starts later, so the two do not run the same phase at the same time
+  if (blockIdx.x >= gridDim.x / 2) {
+    for (int i = 0; i < OMEGA_TP_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
   truepeak_rf_body<K>(p, blockIdx.x, threadIdx.x, smem);
 }
 
@@ -144,17 +165,18 @@ __device__ __forceinline__ void mrfft_rf_body(const SpectralParams& p, int r, in
   const float2* __restrict__ twK = p.tw[ilog2(K)];
   const float2* __restrict__ twM = p.tw[ilog2(M)];
   float2 v[16];
+  const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];  // (issued before the frame: see truepeak_rf_body)
+  const float2 wm = twM[t];
+  asm volatile("" ::: "memory");
   static_for<0, 16>([&](auto q) {
     const float2 a = x2[t + NTH * q], w = w2[t + NTH * q];
     v[q] = make_float2(a.x * w.x, a.y * w.y);
   });
-  const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];
-  const float2 wm = twM[t];
   // this thread's first combine entry, fetched with the frame
   const int e0 = rp.ent_begin + t;
   CombEnt ent{};
   if (p.comb_out && e0 < rp.ent_end) ent = p.ent[e0];
-  FFT::run(v, buf, t, w1, w2b);
+  FFT::template run<false, kRfTab>(v, buf, t, w1, w2b, p.rtw1[K == 8192], p.rtw2[K == 8192]);
   __syncthreads();
   FFT::store_spectrum(v, buf, t);
   __syncthreads();
@@ -213,6 +235,8 @@ __global__ __launch_bounds__(K / 16, 4) void mrfft_rf_kernel(SpectralParams p, i
   mrfft_rf_body<K>(p, r, blockIdx.x, threadIdx.x, smem);
 }
 
+OMEGA_STAMPS_GETTER(omega_debug_rf_stamps)
+
 hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
   if (n == 16384) {
@@ -251,14 +275,15 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   const float2* x2 = reinterpret_cast<const float2*>(p.x + fr * p.stride);
   const float2* w2 = reinterpret_cast<const float2*>(p.win);
   float2 v[16];
+  const float2* __restrict__ twK = p.tw[ilog2(K)];
+  const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];  // (issued before the frame: see truepeak_rf_body)
+  const float2 wm = p.tw[ilog2(2 * K)][t];
+  asm volatile("" ::: "memory");
   static_for<0, 16>([&](auto r) {
     const float2 a = x2[t + NTH * r], w = w2[t + NTH * r];
     v[r] = make_float2(a.x * w.x, a.y * w.y);
   });
-  const float2* __restrict__ twK = p.tw[ilog2(K)];
-  const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];
-  const float2 wm = p.tw[ilog2(2 * K)][t];
-  FFT::run(v, buf, t, w1, w2b);
+  FFT::template run<false, kRfTab>(v, buf, t, w1, w2b, p.rtw1, p.rtw2);
   __syncthreads();
   FFT::store_spectrum(v, buf, t);
   __syncthreads();

@@ -24,7 +24,7 @@ def main(stage):
     lib = L.lib()
     eng._bind_stream(x)
     li = torch.empty(512, device="cuda")
-    getter = {"kw": "omega_debug_kw_stamps", "tp": "omega_debug_spectral_stamps",
+    getter = {"kw": "omega_debug_kw_stamps", "tp": "omega_debug_spectral_stamps", "tprf": "omega_debug_rf_stamps",
               "mrfft": "omega_debug_spectral_stamps", "meters": "omega_debug_meter_stamps",
               "spectra": "omega_debug_spectra_stamps"}[stage]
     if stage == "spectra":
@@ -42,7 +42,7 @@ def main(stage):
     for _ in range(3 if stage != "meters" else 20):
         if stage == "kw":
             eng._check(lib.omega_k_weighting(eng._ctx, x.data_ptr(), 512, 16384, None, li.data_ptr(), L.MEM_DEVICE))
-        elif stage == "tp":
+        elif stage in ("tp", "tprf"):
             eng._check(lib.omega_true_peak(eng._ctx, x.data_ptr(), 512, 16384, li.data_ptr(), L.MEM_DEVICE))
         elif stage == "spectra":
             e3.spectra(x3, "hann", bands=bt, chroma=True)
