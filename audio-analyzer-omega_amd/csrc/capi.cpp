@@ -30,6 +30,7 @@ hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
+hipError_t launch_weight_ac(int m, int mode, const KWeightParams& p, hipStream_t s);
 hipError_t launch_spectra(int m, const SpectraParams& p, int grid, hipStream_t s);
 hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s);
 hipError_t launch_frame(const SpectralParams& sp, const KWeightParams& kp, hipStream_t s);
@@ -89,6 +90,32 @@ double rfreq(int k, int N, double fs) {
 struct BiquadCoef {
   double b[3], a[3];
 };
+
+// scipy.signal.butter(2, fc/(fs/2), 'low') and butter(1, ..., 'high' / 'low') (bilinear, prewarped);
+// first-order sections as biquads with b2 = a2 = 0
+BiquadCoef butter2_lowpass(double fc, double fs) {
+  const double K = std::tan(kPi * fc / fs);
+  const double n = 1.0 + std::sqrt(2.0) * K + K * K;
+  BiquadCoef c;
+  c.b[0] = K * K / n;
+  c.b[1] = 2.0 * K * K / n;
+  c.b[2] = K * K / n;
+  c.a[0] = 1.0;
+  c.a[1] = 2.0 * (K * K - 1.0) / n;
+  c.a[2] = (1.0 - std::sqrt(2.0) * K + K * K) / n;
+  return c;
+}
+BiquadCoef butter1(double fc, double fs, bool high) {
+  const double K = std::tan(kPi * fc / fs);
+  BiquadCoef c;
+  c.b[0] = high ? 1.0 / (1.0 + K) : K / (1.0 + K);
+  c.b[1] = high ? -1.0 / (1.0 + K) : K / (1.0 + K);
+  c.b[2] = 0.0;
+  c.a[0] = 1.0;
+  c.a[1] = (K - 1.0) / (K + 1.0);
+  c.a[2] = 0.0;
+  return c;
+}
 
 // scipy.signal.butter(2, fc/(fs/2), 'high') (bilinear transform, prewarped)
 BiquadCoef butter2_highpass(double fc, double fs) {
@@ -1705,11 +1732,37 @@ int omega_k_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, float*
   return omega_weighting(c, x, n, m, OMEGA_WEIGHT_K, weighted, lufs_inst, mem);
 }
 
+// The A- / C-weighting stage tables for frames of M samples (professional_meters.py:74-127): A =
+// {butter(2, 20.598997 Hz, high), butter(1, 107.65265, high), butter(1, 737.86223, low),
+// butter(2, min(12194.217 / nyq, 0.99), low)}; C = {butter(2, 20.598997, high), butter(2, 12194.217, low)}.
+int get_ac_tabs(omega_ctx* c, int M, int mode, BiquadTab** out) {
+  const int L = kw_chunk(M);
+  const auto key = std::make_pair(M, -mode);  // (negative chunk: not a K table)
+  auto it = c->kw_tabs.find(key);
+  if (it != c->kw_tabs.end()) {
+    *out = it->second;
+    return 0;
+  }
+  const double fs = c->cfg.sample_rate, nyq = fs / 2;
+  const double f1 = 20.598997, f2 = 107.65265, f3 = 737.86223, f4 = 12194.217;
+  const double f4c = std::min(f4 / nyq, 0.99) * nyq;
+  std::vector<BiquadTab> t;
+  if (mode == OMEGA_WEIGHT_A)
+    t = {make_biquad_tab(butter2_highpass(f1, fs), L), make_biquad_tab(butter1(f2, fs, true), L),
+         make_biquad_tab(butter1(f3, fs, false), L), make_biquad_tab(butter2_lowpass(f4c, fs), L)};
+  else
+    t = {make_biquad_tab(butter2_highpass(f1, fs), L), make_biquad_tab(butter2_lowpass(f4c, fs), L)};
+  BiquadTab* d = nullptr;
+  if (int e = upload(c, &d, t)) return e;
+  c->kw_tabs[key] = d;
+  *out = d;
+  return 0;
+}
+
 int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t mode, float* weighted,
                     float* lufs_inst, int mem) {
   if (!c || !x) return OMEGA_EINVAL;
-  if (mode != OMEGA_WEIGHT_K && mode != OMEGA_WEIGHT_Z)
-    return fail(c, OMEGA_EUNSUP, "weighting mode %d: only K and Z are implemented", mode);
+  if (mode < OMEGA_WEIGHT_K || mode > OMEGA_WEIGHT_Z) return fail(c, OMEGA_EINVAL, "weighting mode %d", mode);
   if (!is_pow2_in(m, 512, 16384)) return fail(c, OMEGA_EUNSUP, "k-weighting: frame length %d unsupported", m);
   if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
   HIPC(c, hipSetDevice(c->device));
@@ -1725,10 +1778,17 @@ int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t 
     if (e) return e;
   }
   BiquadTab* tabs = nullptr;
-  e = get_kw_tab(c, m, &tabs);
-  if (e) return e;
-  KWeightParams kp{dx, m, 0, 1, n, tabs, tabs + 1, dl, dw, mode};
-  HIPC(c, launch_kweight(m, kp, c->stream));
+  if (mode == OMEGA_WEIGHT_A || mode == OMEGA_WEIGHT_C) {
+    e = get_ac_tabs(c, m, mode, &tabs);
+    if (e) return e;
+    KWeightParams kp{dx, m, 0, 1, n, tabs, nullptr, dl, dw, mode};
+    HIPC(c, launch_weight_ac(m, mode, kp, c->stream));
+  } else {
+    e = get_kw_tab(c, m, &tabs);
+    if (e) return e;
+    KWeightParams kp{dx, m, 0, 1, n, tabs, tabs + 1, dl, dw, mode};
+    HIPC(c, launch_kweight(m, kp, c->stream));
+  }
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 }

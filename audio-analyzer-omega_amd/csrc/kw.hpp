@@ -229,19 +229,20 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
 }
 
 // filtfilt of the block-distributed signal u (in place). e[0..9] = u[0..9], e[10..19] = u[M-10..M-1].
-template <int L, int NTH, int SB, bool OPQ = false>
+// E: scipy's padlen 3 max(len(a), len(b)) -- 9 for a biquad, 6 for a first-order section (b2 = a2 = 0)
+template <int L, int NTH, int SB, bool OPQ = false, int E = 9>
 __device__ __forceinline__ void filtfilt(float (&u)[L], const BiquadTab* __restrict__ tg, const float4* pwl, const float* e,
                                          float* sh, int tid) {
-  constexpr int E = 9;
+  static_assert(E >= 1 && E <= 9, "the gathered edges cover 10 samples per side");
   const BqRegs t = bq_regs(tg);
-  // left odd extension ext[i] = 2u[0] - u[9-i], i < 9 (formed in float32, as scipy does for f32)
+  // left odd extension ext[i] = 2u[0] - u[E-i], i < E (formed in float32, as scipy does for f32)
   const float u0 = e[0], uN = e[19];
   float s0 = t.zi0 * (2.f * u0 - e[E]), s1 = t.zi1 * (2.f * u0 - e[E]);
 #pragma unroll
   for (int i = 0; i < E; ++i) bq_step(t, 2.f * u0 - e[E - i], s0, s1);
   float f0, f1;
   lfilter_pass<L, NTH, false, SB, OPQ>(u, t, pwl, s0, s1, sh, tid, f0, f1);
-  // right odd extension ext[M+9+i] = 2u[M-1] - u[M-2-i]: forward outputs, then the backward start
+  // right odd extension ext[M+E+i] = 2u[M-1] - u[M-2-i]: forward outputs, then the backward start
   float yr[E];
 #pragma unroll
   for (int i = 0; i < E; ++i) yr[i] = bq_step(t, 2.f * uN - e[18 - i], f0, f1);
@@ -369,6 +370,60 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
   const double ms = block_sum_f<NTH>(acc, red, tid) / M;
   if (tid == 0 && p.lufs_out) put_lufs<PUB>(p.lufs_out, cf, ms > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms)) : -100.0f);
   OMEGA_STAMP(26);
+}
+
+// A- and C-weighting (professional_meters.py:74-127, :155-218): cascaded filtfilt stages on the
+// register-resident frame -- A: 2nd-order high-pass 20.6 Hz, 1st-order high-pass 107.7 Hz, 1st-order
+// low-pass 737.9 Hz, 2nd-order low-pass 12194 Hz, times 2.5 (:188); C: 2nd-order high-pass 20.6 Hz,
+// 2nd-order low-pass 12194 Hz -- with the same RMS gate and the instantaneous LUFS of the weighted
+// signal. tabs: the stages' scan tables (host, in order); pwl: LDS [4][kPwl].
+template <int M, int NTH, int MODE>
+__device__ __forceinline__ void weight_chain_body(const KWeightParams& p, const BiquadTab* __restrict__ tabs, int64_t cf,
+                                                  int tid, float4 (*pwl)[kPwl], float* sh, float* edge, double* red) {
+  constexpr int L = M / NTH;
+  constexpr int NS = MODE == 1 ? 4 : 2;
+  const int64_t f = cf / p.C, c = cf % p.C;
+  const float* __restrict__ x = p.x + f * p.frame_stride + c * p.chan_stride;
+  for (int i = tid; i < NS * kPwl; i += NTH) {
+    const BiquadTab& t = tabs[i / kPwl];
+    const int l = i % kPwl;
+    pwl[i / kPwl][l] = l < 64 ? make_float4(t.pw[l][0], t.pw[l][1], t.pw[l][2], t.pw[l][3])
+                              : make_float4(t.h0[l - 64], t.h1[l - 64], 0.f, 0.f);
+  }
+  float u[L];
+  static_for<0, L>([&](auto i) { u[i] = x[tid * L + i]; });
+  float ss = 0.f;
+  static_for<0, L>([&](auto i) { ss = fmaf(u[i], u[i], ss); });
+  const double ms_in = block_sum_f<NTH>(ss, red, tid) / M;
+  float* wout = p.weighted_out ? p.weighted_out + cf * M + tid * L : nullptr;
+  if (sqrt(ms_in) < 1e-6) {  // :158-160, :198-200
+    if (wout) static_for<0, L>([&](auto i) { wout[i] = 0.f; });
+    if (tid == 0 && p.lufs_out) p.lufs_out[cf] = -100.0f;
+    return;
+  }
+  auto stage = [&](auto si, auto E) {
+    gather_edges<L, NTH>(u, edge, tid);
+    __syncthreads();
+    filtfilt<L, NTH, 4, false, decltype(E)::value>(u, tabs + si, pwl[si], edge, sh, tid);
+    __syncthreads();  // the edges are read again by the next stage
+  };
+  using E9 = std::integral_constant<int, 9>;
+  using E6 = std::integral_constant<int, 6>;
+  if constexpr (MODE == 1) {
+    stage(std::integral_constant<int, 0>{}, E9{});
+    stage(std::integral_constant<int, 1>{}, E6{});
+    stage(std::integral_constant<int, 2>{}, E6{});
+    stage(std::integral_constant<int, 3>{}, E9{});
+    static_for<0, L>([&](auto i) { u[i] = u[i] * 2.5f; });  // filtered *= 2.5 (:188)
+  } else {
+    stage(std::integral_constant<int, 0>{}, E9{});
+    stage(std::integral_constant<int, 1>{}, E9{});
+  }
+  float acc = 0.f;
+  static_for<0, L>([&](auto i) { acc = fmaf(u[i], u[i], acc); });
+  if (wout) static_for<0, L>([&](auto i) { wout[i] = u[i]; });
+  const double ms = block_sum_f<NTH>(acc, red, tid) / M;
+  if (tid == 0 && p.lufs_out) p.lufs_out[cf] = ms > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms)) : -100.0f;
 }
 
 }  // namespace omega

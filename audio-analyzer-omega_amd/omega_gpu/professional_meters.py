@@ -33,6 +33,18 @@ def _butter2_highpass(fc: float, fs: float):
     return np.array([1.0, -2.0, 1.0]) / n, np.array([1.0, 2 * (k * k - 1) / n, (1 - np.sqrt(2) * k + k * k) / n])
 
 
+def _butter2_lowpass(fc: float, fs: float):
+    k = np.tan(np.pi * fc / fs)
+    n = 1 + np.sqrt(2) * k + k * k
+    return np.array([k * k, 2 * k * k, k * k]) / n, np.array([1.0, 2 * (k * k - 1) / n, (1 - np.sqrt(2) * k + k * k) / n])
+
+
+def _butter1(fc: float, fs: float, high: bool):
+    k = np.tan(np.pi * fc / fs)
+    b = np.array([1.0, -1.0]) / (1 + k) if high else np.array([k, k]) / (1 + k)
+    return b, np.array([1.0, (k - 1) / (k + 1)])
+
+
 class ProfessionalMetering:
     """Professional audio metering standards (LUFS, K-weighting, True Peak)."""
 
@@ -47,6 +59,8 @@ class ProfessionalMetering:
         self.current_lufs = {"momentary": -100.0, "short_term": -100.0, "integrated": -100.0, "range": 0.0,
                              "true_peak": -100.0}
         self.current_true_peak = -100.0
+        self.a_weighting_filter = self.create_a_weighting_filter()
+        self.c_weighting_filter = self.create_c_weighting_filter()
         # one context: its meter state is the four deques of :20-25 for one stream
         self._eng = Engine([Resolution((20, 20000), 512, 256, 1.0)], sample_rate, min(20000, sample_rate / 2),
                            target_bins=2, frame_size=512, n_channels=1, device=device)
@@ -59,22 +73,43 @@ class ProfessionalMetering:
 
     def apply_k_weighting(self, audio_data: np.ndarray) -> np.ndarray:
         """professional_meters.py:129-153 (returned as float64 like scipy's filtfilt)."""
+        return self._weighted(audio_data, "K")
+
+    def create_a_weighting_filter(self):
+        """professional_meters.py:74-107: the four cascaded Butterworth sections (the device builds the
+        same coefficients in omega_weighting)."""
+        fs, nyq = self.sample_rate, self.sample_rate / 2
+        return {"hp1": _butter2_highpass(20.598997, fs), "hp2": _butter1(107.65265, fs, True),
+                "lp1": _butter1(737.86223, fs, False), "lp2": _butter2_lowpass(min(12194.217 / nyq, 0.99) * nyq, fs),
+                "gain": 1.0}
+
+    def create_c_weighting_filter(self):
+        """professional_meters.py:109-127."""
+        fs, nyq = self.sample_rate, self.sample_rate / 2
+        return {"hp": _butter2_highpass(20.598997, fs), "lp": _butter2_lowpass(min(12194.217 / nyq, 0.99) * nyq, fs),
+                "gain": 1.0}
+
+    def _weighted(self, audio_data, mode: str) -> np.ndarray:
         try:
-            w, _ = self._eng.weighting(self._frame(audio_data), "K")
+            w, _ = self._eng.weighting(self._frame(audio_data), mode)
             return w[0].astype(np.float64)
         except Exception as e:
-            logger.error("apply_k_weighting: %s", e)
+            logger.error("apply_%s_weighting: %s", mode.lower(), e)
             return np.zeros(len(audio_data), np.float64)
 
+    def apply_a_weighting(self, audio_data: np.ndarray) -> np.ndarray:
+        """professional_meters.py:155-192: RMS gate, four cascaded filtfilt sections, times 2.5."""
+        return self._weighted(audio_data, "A")
+
+    def apply_c_weighting(self, audio_data: np.ndarray) -> np.ndarray:
+        """professional_meters.py:194-218: RMS gate, two cascaded filtfilt sections."""
+        return self._weighted(audio_data, "C")
+
     def apply_weighting(self, audio_data: np.ndarray) -> np.ndarray:
-        """professional_meters.py:220-229: K and Z are implemented on the device; A and C are logged
-        and give zeros (in the reference app only K is reachable: SURVEY.md §8(a) A7)."""
-        if self.weighting_mode == "Z" or self.weighting_mode not in ("K", "A", "C"):
+        """professional_meters.py:220-229: K, A and C on the device; any other mode is Z (unweighted)."""
+        if self.weighting_mode not in ("K", "A", "C"):
             return audio_data
-        if self.weighting_mode != "K":
-            logger.error("apply_weighting: weighting mode %s not implemented on the device", self.weighting_mode)
-            return np.zeros(len(audio_data), np.float64)
-        return self.apply_k_weighting(audio_data)
+        return self._weighted(audio_data, self.weighting_mode)
 
     def calculate_true_peak(self, audio_data: np.ndarray, oversampling: int = 4) -> float:
         """professional_meters.py:283-299 (float32 result for float32 input, like scipy)."""
@@ -109,7 +144,8 @@ class ProfessionalMetering:
     def calculate_lufs_batch(self, frames: np.ndarray) -> np.ndarray:
         """Batched form: frames [F, M] of one stream in order -> [F, 5] dict values per call."""
         frames = np.ascontiguousarray(frames, dtype=np.float32)
-        _, li = self._eng.weighting(frames, "K", weighted=False)
+        mode = "Z" if self.weighting_mode not in ("K", "A", "C") else self.weighting_mode
+        _, li = self._eng.weighting(frames, mode, weighted=False)
         tp = self._eng.true_peak(frames)
         return self._eng.meter_update(li, tp, frames.shape[0])
 

@@ -160,7 +160,9 @@ int omega_k_weighting(omega_ctx* ctx, const float* x, int64_t n, int32_t m, floa
                       float* lufs_inst, int mem);
 
 /* apply_weighting + instantaneous LUFS for a weighting mode (professional_meters.py:220-229):
- * K (0) and Z (3: the signal itself, no gate) are implemented; A (1) and C (2) return OMEGA_EUNSUP. */
+ * K (0, :129-153), A (1, :155-192: four cascaded Butterworth filtfilt sections, x 2.5), C (2, :194-218:
+ * two sections) and Z (3: the signal itself, no gate). The A and C coefficients are built for the
+ * context's sample rate (create_a/c_weighting_filter, :74-127). */
 typedef enum { OMEGA_WEIGHT_K = 0, OMEGA_WEIGHT_A = 1, OMEGA_WEIGHT_C = 2, OMEGA_WEIGHT_Z = 3 } omega_weighting_mode;
 int omega_weighting(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t mode, float* weighted,
                     float* lufs_inst, int mem);

@@ -379,6 +379,36 @@ def gen_transients(R):
     np.savez_compressed(os.path.join(OUT, "transients.npz"), **d)
 
 
+def gen_weighting_ac(R):
+    """apply_a_weighting / apply_c_weighting outputs and calculate_lufs sequences with
+    weighting_mode 'A' and 'C' (professional_meters.py:155-229), at 48 kHz and 44.1 kHz."""
+    d = {"versions": VERSIONS}
+    sigs = {"sine2048": S.sine(1000, 0.1, 2048), "comp4800": S.composite(4800),
+            "hann2048_f64": S.composite(2048) * np.hanning(2048), "low50_4096": S.sine(50, 0.5, 4096),
+            "noise16384": S.noise(12, 16384, 0.2), "quiet1024": S.sine(440, 5e-7, 1024)}
+    for fs in (48000, 44100):
+        pm = R.ProfessionalMetering(fs)
+        for name, x in sigs.items():
+            d[f"{fs}/{name}/x"] = x
+            d[f"{fs}/{name}/A"] = pm.apply_a_weighting(x)
+            d[f"{fs}/{name}/C"] = pm.apply_c_weighting(x)
+        for k in ("hp1", "hp2", "lp1", "lp2"):
+            d[f"{fs}/coefA/{k}/b"], d[f"{fs}/coefA/{k}/a"] = pm.a_weighting_filter[k]
+        for k in ("hp", "lp"):
+            d[f"{fs}/coefC/{k}/b"], d[f"{fs}/coefC/{k}/a"] = pm.c_weighting_filter[k]
+    frames = (S.sine(997, 0.25, 30 * 2048) + S.noise(13, 30 * 2048, 0.02)).reshape(30, 2048)
+    d["seq/x"] = frames
+    for mode in ("A", "C"):
+        pm = R.ProfessionalMetering(FS)
+        pm.weighting_mode = mode
+        agg = []
+        for x in frames:
+            r = pm.calculate_lufs(x)
+            agg.append([r[k] for k in ("momentary", "short_term", "integrated", "range", "true_peak")])
+        d[f"seq/{mode}/agg"] = np.array(agg, np.float64)
+    np.savez_compressed(os.path.join(OUT, "weighting_ac.npz"), **d)
+
+
 def gen_batched(R):
     d = {"versions": VERSIONS}
     bp = R.BatchedFFTProcessor()
@@ -544,6 +574,6 @@ if __name__ == "__main__":
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients"))]:
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac"))]:
         g(R)
         print("wrote", g.__name__)

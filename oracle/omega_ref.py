@@ -261,9 +261,42 @@ def apply_k_weighting(x: np.ndarray, fs: float = 48000) -> np.ndarray:
     return f + (s - f) * 0.3
 
 
+def ac_weighting_coeffs(fs: float = 48000, mode: str = "A"):
+    """professional_meters.py:74-127: A = butter(2, 20.598997, 'high'), butter(1, 107.65265, 'high'),
+    butter(1, 737.86223, 'low'), butter(2, min(12194.217 / nyq, 0.99), 'low'); C = the first and last."""
+    nyq = fs / 2
+    hp1 = _sig.butter(2, 20.598997 / nyq, btype="high")
+    lp2 = _sig.butter(2, min(12194.217 / nyq, 0.99), btype="low")
+    if mode == "C":
+        return [hp1, lp2]
+    return [hp1, _sig.butter(1, 107.65265 / nyq, btype="high"), _sig.butter(1, 737.86223 / nyq, btype="low"), lp2]
+
+
+def apply_ac_weighting(x: np.ndarray, fs: float = 48000, mode: str = "A") -> np.ndarray:
+    """professional_meters.py:155-192 (A: cascaded filtfilt, then *= 2.5) and :194-218 (C)."""
+    x = np.asarray(x)
+    if np.sqrt(np.mean(x ** 2)) < 1e-6:
+        return np.zeros_like(x)
+    y = x.copy()
+    for b, a in ac_weighting_coeffs(fs, mode):
+        y = filtfilt(b, a, y)
+    if mode == "A":
+        y *= 2.5
+    return y
+
+
+def apply_weighting(x: np.ndarray, fs: float = 48000, mode: str = "K") -> np.ndarray:
+    """professional_meters.py:220-229."""
+    if mode == "K":
+        return apply_k_weighting(x, fs)
+    if mode in ("A", "C"):
+        return apply_ac_weighting(x, fs, mode)
+    return np.asarray(x)
+
+
 def lufs_instant(x: np.ndarray, fs: float = 48000, weighting: str = "K") -> float:
     """professional_meters.py:236-246 (instantaneous part of calculate_lufs)."""
-    y = apply_k_weighting(x, fs) if weighting == "K" else np.asarray(x)
+    y = apply_weighting(x, fs, weighting)
     ms = np.mean(y ** 2)
     return float(-0.691 + 10 * np.log10(ms)) if ms > 1e-10 else -100.0
 

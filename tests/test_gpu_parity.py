@@ -226,7 +226,7 @@ def test_meter_unsupported_length_keeps_state():
 def test_true_peak_oversampling(m):
     """calculate_true_peak(x, oversampling) for 1, 2 and 4 (phase subsets of the polyphase transform)
     against scipy's resample (the oracle); an unsupported factor is logged and the previous value
-    returned; apply_weighting in an unimplemented mode logs and gives zeros (no exception)."""
+    returned."""
     from omega_gpu.professional_meters import ProfessionalMetering
     pm = ProfessionalMetering(FS)
     x = S.sine(997, 0.4, m) + S.noise(31, m, 0.05)
@@ -236,8 +236,53 @@ def test_true_peak_oversampling(m):
     assert pm.calculate_true_peak(x, 4) > pm.calculate_true_peak(x, 2) - 1e-6 > pm.calculate_true_peak(x, 1) - 2e-6
     prev = pm.calculate_true_peak(x, 4)
     assert pm.calculate_true_peak(x, 3) == prev
-    pm.weighting_mode = "A"
-    assert not pm.apply_weighting(x).any()
+
+
+@pytest.mark.parametrize("fs", [48000, 44100])
+@pytest.mark.parametrize("mode", ["A", "C"])
+def test_ac_weighting_golden(fs, mode):
+    """apply_a_weighting / apply_c_weighting (professional_meters.py:155-218) on the device: cascaded
+    filtfilt sections (first-order ones with scipy's padlen 6) in the register-resident chunked scan,
+    against the reference's float64 outputs. The 20.6 Hz high-pass pole sits at radius 0.9981 (48 kHz),
+    closer to the unit circle than K-weighting's 38 Hz: the float32 scan carries ~1e-3 normwise error;
+    the bar that matters is the LUFS (0.1 LU) of the weighted signal."""
+    from omega_gpu.professional_meters import ProfessionalMetering
+    g = load_golden("weighting_ac")
+    pm = ProfessionalMetering(fs)
+    for name in ("sine2048", "hann2048_f64", "low50_4096", "noise16384", "quiet1024"):
+        x = g[f"{fs}/{name}/x"]
+        y = pm.apply_a_weighting(x) if mode == "A" else pm.apply_c_weighting(x)
+        ref = g[f"{fs}/{name}/{mode}"]
+        assert y.dtype == np.float64 and y.shape == ref.shape
+        if not ref.any():
+            assert not y.any(), name  # RMS gate
+            continue
+        assert normwise(y, ref) < 5e-3, (name, normwise(y, ref))
+        lu = 10 * np.log10(np.mean(y ** 2)) - 10 * np.log10(np.mean(ref ** 2))
+        assert abs(lu) < 0.01, (name, lu)
+    pm.weighting_mode = mode
+    x = g[f"{fs}/sine2048/x"]
+    np.testing.assert_array_equal(pm.apply_weighting(x), pm.apply_a_weighting(x) if mode == "A" else pm.apply_c_weighting(x))
+
+
+@pytest.mark.parametrize("mode", ["A", "C"])
+def test_ac_weighting_lufs_sequence(mode):
+    """calculate_lufs with weighting_mode A / C (the panel's mode switch, professional_meters.py:552)
+    against the reference's aggregate dicts, frame by frame and batched."""
+    from omega_gpu.professional_meters import ProfessionalMetering
+    g = load_golden("weighting_ac")
+    agg = g[f"seq/{mode}/agg"]
+    pm = ProfessionalMetering(FS)
+    pm.weighting_mode = mode
+    for f, x in enumerate(g["seq/x"]):
+        d = pm.calculate_lufs(x)
+        got = np.array([d[k] for k in ("momentary", "short_term", "integrated", "range", "true_peak")])
+        assert np.all(np.abs(got[:4] - agg[f, :4]) < LU_TOL), (f, got, agg[f])
+        assert abs(got[4] - agg[f, 4]) < TP_TOL_DB
+    pm2 = ProfessionalMetering(FS)
+    pm2.weighting_mode = mode
+    out = pm2.calculate_lufs_batch(g["seq/x"])
+    assert np.max(np.abs(out[:, :4] - agg[:, :4])) < LU_TOL
 
 
 def test_bands_golden(golden):

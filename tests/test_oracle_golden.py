@@ -97,6 +97,41 @@ def test_k_weighting_signal(me, name):
     assert abs(R.true_peak(me[f"kw/{name}/x"]) - me[f"kw/{name}/tp"]) < 1e-5
 
 
+@pytest.mark.parametrize("fs", [48000, 44100])
+def test_ac_weighting_oracle(fs):
+    """A / C weighting (professional_meters.py:74-218): the oracle's cascade against the reference's
+    outputs, and the facade's closed-form Butterworth sections against scipy's coefficients."""
+    g = load_golden("weighting_ac")
+    for name in ("sine2048", "comp4800", "hann2048_f64", "low50_4096", "noise16384", "quiet1024"):
+        x = g[f"{fs}/{name}/x"]
+        for mode in ("A", "C"):
+            np.testing.assert_allclose(R.apply_ac_weighting(x, fs, mode), g[f"{fs}/{name}/{mode}"], rtol=1e-12, atol=1e-14)
+    assert not g[f"{fs}/quiet1024/A"].any()  # the RMS gate
+    from omega_gpu import professional_meters as P
+    nyq = fs / 2
+    closed = {"coefA/hp1": P._butter2_highpass(20.598997, fs), "coefA/hp2": P._butter1(107.65265, fs, True),
+              "coefA/lp1": P._butter1(737.86223, fs, False),
+              "coefA/lp2": P._butter2_lowpass(min(12194.217 / nyq, 0.99) * nyq, fs),
+              "coefC/hp": P._butter2_highpass(20.598997, fs), "coefC/lp": P._butter2_lowpass(min(12194.217 / nyq, 0.99) * nyq, fs)}
+    for k, (b, a) in closed.items():
+        np.testing.assert_allclose(b, g[f"{fs}/{k}/b"], rtol=1e-9, atol=1e-15)
+        np.testing.assert_allclose(a, g[f"{fs}/{k}/a"], rtol=1e-9, atol=1e-15)
+    for (b, a), k in zip(R.ac_weighting_coeffs(fs, "A"), ("hp1", "hp2", "lp1", "lp2")):
+        np.testing.assert_array_equal(b, g[f"{fs}/coefA/{k}/b"])
+
+
+def test_ac_weighting_lufs_sequence():
+    """calculate_lufs with weighting_mode A / C: the oracle's meter state over the reference's frames."""
+    g = load_golden("weighting_ac")
+    for mode in ("A", "C"):
+        st = R.MeterState(FS)
+        for f, x in enumerate(g["seq/x"]):
+            r = st.update(x, R.lufs_instant(x, FS, mode), R.true_peak(x))
+            got = np.array(list(r.values()), np.float64)
+            np.testing.assert_allclose(got[:4], g[f"seq/{mode}/agg"][f, :4], rtol=1e-9, atol=1e-9)
+            assert abs(got[4] - g[f"seq/{mode}/agg"][f, 4]) < 1e-5  # float32 true peak (scipy's resample), 1 ulp
+
+
 def test_filtfilt_restatement_matches_scipy():
     import scipy.signal as ss
     x = S.noise(3, 3000, 0.3).astype(np.float64)
