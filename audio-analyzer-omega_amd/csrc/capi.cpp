@@ -30,7 +30,8 @@ hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
-hipError_t launch_weight_ac(int m, int mode, const KWeightParams& p, hipStream_t s);
+hipError_t launch_weight64(const Weight64Params& p, hipStream_t s);
+hipError_t launch_any(const AnyFftParams& p, int truepeak, hipStream_t s);
 hipError_t launch_spectra(int m, const SpectraParams& p, int grid, hipStream_t s);
 hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s);
 hipError_t launch_frame(const SpectralParams& sp, const KWeightParams& kp, hipStream_t s);
@@ -282,6 +283,19 @@ struct omega_ctx {
   std::map<int, std::pair<double2*, double2*>> tr_tw;
   double* d_sg = nullptr;
   int64_t dflux_cap = 0;
+  // omega_weighting: float64 filter cascades per mode and the per-launch working buffers
+  W64Stage* w64[4] = {};
+  // frames of any length (anyfft.hip): per N the radices and the twiddle / rotation tables
+  struct AnyPlan {
+    std::vector<int> radix;
+    float2* tw = nullptr;
+    float2* rot = nullptr;
+  };
+  std::map<int, AnyPlan> any_plans;
+  float2* d_any = nullptr;
+  int64_t any_cap = 0;
+  double* d_w64 = nullptr;
+  int64_t w64_cap = 0;
   // meter state (double-buffered)
   float* d_hist_l[2] = {};
   float* d_hist_t[2] = {};
@@ -1689,13 +1703,74 @@ int omega_true_peak(omega_ctx* c, const float* x, int64_t n, int32_t m, float* o
   return omega_true_peak_os(c, x, n, m, 4, out_db, mem);
 }
 
+// Plan of the any-length transform: radices (4s, then 2, 3, 5, 7, then the remaining primes) and the
+// tables e^{-2 pi i m / N}, e^{2 pi i m / (4N)} in float64 rounded to float32
+int get_any_plan(omega_ctx* c, int N, omega_ctx::AnyPlan** out) {
+  auto it = c->any_plans.find(N);
+  if (it == c->any_plans.end()) {
+    omega_ctx::AnyPlan pl;
+    int r = N;
+    while (r % 4 == 0) pl.radix.push_back(4), r /= 4;
+    for (int f : {2, 3, 5, 7})
+      while (r % f == 0) pl.radix.push_back(f), r /= f;
+    for (int f = 11; (int64_t)f * f <= r; f += 2)
+      while (r % f == 0) pl.radix.push_back(f), r /= f;
+    if (r > 1) pl.radix.push_back(r);
+    if ((int)pl.radix.size() > kAnyMaxStages) return fail(c, OMEGA_EUNSUP, "length %d: too many factors", N);
+    std::vector<float2> tw(N), rot(3 * (N / 2) + 1);
+    for (int m = 0; m < N; ++m) tw[m] = make_float2((float)std::cos(2 * kPi * m / N), (float)-std::sin(2 * kPi * m / N));
+    for (size_t m = 0; m < rot.size(); ++m)
+      rot[m] = make_float2((float)std::cos(2 * kPi * (double)m / (4.0 * N)), (float)std::sin(2 * kPi * (double)m / (4.0 * N)));
+    int e = upload(c, &pl.tw, tw);
+    if (!e) e = upload(c, &pl.rot, rot);
+    if (e) return e;
+    it = c->any_plans.emplace(N, std::move(pl)).first;
+  }
+  *out = &it->second;
+  return 0;
+}
+
+// launches the any-length kernel over n frames in slices whose global scratch (N > kAnyLdsMax) stays
+// within 64 MiB; p.x / outputs advanced per slice
+int run_any(omega_ctx* c, AnyFftParams p, int truepeak) {
+  omega_ctx::AnyPlan* pl = nullptr;
+  if (int e = get_any_plan(c, p.N, &pl)) return e;
+  p.n_stages = (int)pl->radix.size();
+  for (int s = 0; s < p.n_stages; ++s) p.radix[s] = pl->radix[s];
+  p.tw = pl->tw;
+  p.rot = pl->rot;
+  for (int ph = 0; ph < 4; ++ph) p.nyq_cos[ph] = (float)std::cos(kPi * ph / 4.0);
+  const int64_t n = p.n;
+  int64_t per = n;
+  if (p.N > kAnyLdsMax) {
+    per = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)(8 << 20) / (3 * (int64_t)p.N)));
+    if (per * 3 * p.N > c->any_cap) {
+      if (int e = dalloc(c, &c->d_any, (size_t)(per * 3 * p.N))) return e;
+      c->any_cap = per * 3 * p.N;
+    }
+    p.scratch = c->d_any;
+  }
+  const int nb = p.N / 2 + 1;
+  for (int64_t f0 = 0; f0 < n; f0 += per) {
+    AnyFftParams q = p;
+    q.x = p.x + f0 * p.frame_stride;
+    q.n = std::min(per, n - f0);
+    if (q.tp_out) q.tp_out = p.tp_out + f0;
+    if (q.mag) q.mag = p.mag + f0 * nb;
+    if (q.cplx) q.cplx = p.cplx + f0 * nb * 2;
+    HIPC(c, launch_any(q, truepeak, c->stream));
+  }
+  return 0;
+}
+
 int omega_true_peak_os(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t oversampling, float* out_db,
                        int mem) {
   if (!c || !x || !out_db) return OMEGA_EINVAL;
   if (oversampling != 1 && oversampling != 2 && oversampling != 4)
     return fail(c, OMEGA_EUNSUP, "true peak: oversampling %d unsupported (1, 2, 4)", oversampling);
-  if (!is_pow2_in(m, 512, 16384)) return fail(c, OMEGA_EUNSUP, "true peak: frame length %d unsupported", m);
+  if (m < 1) return fail(c, OMEGA_EINVAL, "true peak: frame length %d", m);
   if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  const bool any = !is_pow2_in(m, 512, 16384);
   HIPC(c, hipSetDevice(c->device));
   std::vector<HostOut> outs;
   const float* dx = x;
@@ -1705,6 +1780,18 @@ int omega_true_peak_os(omega_ctx* c, const float* x, int64_t n, int32_t m, int32
     e = stage_in(c, 0, x, (size_t)n * m * sizeof(float), reinterpret_cast<const void**>(&dx));
     if (!e) e = stage_out(c, 3, out_db, n, outs, &dout);
     if (e) return e;
+  }
+  if (any) {  // frames of other lengths (anyfft.hip)
+    AnyFftParams ap{};
+    ap.x = dx;
+    ap.frame_stride = m;
+    ap.n = n;
+    ap.N = m;
+    ap.phases = oversampling == 4 ? 0xE : (oversampling == 2 ? 0x4 : 0);
+    ap.tp_out = dout;
+    if ((e = run_any(c, ap, 1))) return e;
+    if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+    return 0;
   }
   SpectralParams sp = spectral_params(c);
   sp.x = dx;
@@ -1727,42 +1814,10 @@ int omega_true_peak_os(omega_ctx* c, const float* x, int64_t n, int32_t m, int32
   return 0;
 }
 
+// the batch kernel's float32 K-weighting (kweight_kernel) on its own, for power-of-two frames
 int omega_k_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, float* weighted, float* lufs_inst,
                       int mem) {
-  return omega_weighting(c, x, n, m, OMEGA_WEIGHT_K, weighted, lufs_inst, mem);
-}
-
-// The A- / C-weighting stage tables for frames of M samples (professional_meters.py:74-127): A =
-// {butter(2, 20.598997 Hz, high), butter(1, 107.65265, high), butter(1, 737.86223, low),
-// butter(2, min(12194.217 / nyq, 0.99), low)}; C = {butter(2, 20.598997, high), butter(2, 12194.217, low)}.
-int get_ac_tabs(omega_ctx* c, int M, int mode, BiquadTab** out) {
-  const int L = kw_chunk(M);
-  const auto key = std::make_pair(M, -mode);  // (negative chunk: not a K table)
-  auto it = c->kw_tabs.find(key);
-  if (it != c->kw_tabs.end()) {
-    *out = it->second;
-    return 0;
-  }
-  const double fs = c->cfg.sample_rate, nyq = fs / 2;
-  const double f1 = 20.598997, f2 = 107.65265, f3 = 737.86223, f4 = 12194.217;
-  const double f4c = std::min(f4 / nyq, 0.99) * nyq;
-  std::vector<BiquadTab> t;
-  if (mode == OMEGA_WEIGHT_A)
-    t = {make_biquad_tab(butter2_highpass(f1, fs), L), make_biquad_tab(butter1(f2, fs, true), L),
-         make_biquad_tab(butter1(f3, fs, false), L), make_biquad_tab(butter2_lowpass(f4c, fs), L)};
-  else
-    t = {make_biquad_tab(butter2_highpass(f1, fs), L), make_biquad_tab(butter2_lowpass(f4c, fs), L)};
-  BiquadTab* d = nullptr;
-  if (int e = upload(c, &d, t)) return e;
-  c->kw_tabs[key] = d;
-  *out = d;
-  return 0;
-}
-
-int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t mode, float* weighted,
-                    float* lufs_inst, int mem) {
   if (!c || !x) return OMEGA_EINVAL;
-  if (mode < OMEGA_WEIGHT_K || mode > OMEGA_WEIGHT_Z) return fail(c, OMEGA_EINVAL, "weighting mode %d", mode);
   if (!is_pow2_in(m, 512, 16384)) return fail(c, OMEGA_EUNSUP, "k-weighting: frame length %d unsupported", m);
   if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
   HIPC(c, hipSetDevice(c->device));
@@ -1778,16 +1833,94 @@ int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t 
     if (e) return e;
   }
   BiquadTab* tabs = nullptr;
-  if (mode == OMEGA_WEIGHT_A || mode == OMEGA_WEIGHT_C) {
-    e = get_ac_tabs(c, m, mode, &tabs);
+  if ((e = get_kw_tab(c, m, &tabs))) return e;
+  KWeightParams kp{dx, m, 0, 1, n, tabs, tabs + 1, dl, dw, OMEGA_WEIGHT_K};
+  HIPC(c, launch_kweight(m, kp, c->stream));
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+}
+
+// The float64 filter cascade of a weighting mode for the context's sample rate
+// (professional_meters.py:48-72, :74-127): K = {butter(2, 38 Hz, high), iirfilter(2, 1500 Hz, high)}
+// blended 0.3; A = {butter(2, 20.598997, high), butter(1, 107.65265, high), butter(1, 737.86223, low),
+// butter(2, min(12194.217 / nyq, 0.99), low)} x 2.5; C = {butter(2, 20.598997, high), butter(2, 12194.217, low)}.
+W64Stage w64_stage(const BiquadCoef& q, int order) {
+  W64Stage s{};
+  s.b0 = q.b[0];
+  s.b1 = q.b[1];
+  s.b2 = q.b[2];
+  s.a1 = q.a[1];
+  s.a2 = q.a[2];
+  // scipy.signal.lfilter_zi: solve (I - companion(a).T) zi = b[1:] - a[1:] b[0]
+  const double B0 = s.b1 - s.a1 * s.b0, B1 = s.b2 - s.a2 * s.b0;
+  s.zi0 = (B0 + B1) / (1.0 + s.a1 + s.a2);
+  s.zi1 = B1 - s.a2 * s.zi0;
+  s.E = 3 * (order + 1);  // filtfilt's default padlen 3 max(len(a), len(b))
+  return s;
+}
+
+int get_w64_stages(omega_ctx* c, int mode, W64Stage** out) {
+  if (c->w64[mode]) {
+    *out = c->w64[mode];
+    return 0;
+  }
+  const double fs = c->cfg.sample_rate, nyq = fs / 2;
+  const double f1 = 20.598997, f2 = 107.65265, f3 = 737.86223, f4 = 12194.217;
+  const double f4c = std::min(f4 / nyq, 0.99) * nyq;
+  std::vector<W64Stage> t;
+  if (mode == OMEGA_WEIGHT_K)
+    t = {w64_stage(butter2_highpass(38.0, fs), 2), w64_stage(butter2_highpass(1500.0, fs), 2)};
+  else if (mode == OMEGA_WEIGHT_A)
+    t = {w64_stage(butter2_highpass(f1, fs), 2), w64_stage(butter1(f2, fs, true), 1),
+         w64_stage(butter1(f3, fs, false), 1), w64_stage(butter2_lowpass(f4c, fs), 2)};
+  else
+    t = {w64_stage(butter2_highpass(f1, fs), 2), w64_stage(butter2_lowpass(f4c, fs), 2)};
+  if (int e = upload(c, &c->w64[mode], t)) return e;
+  *out = c->w64[mode];
+  return 0;
+}
+
+int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t mode, float* weighted,
+                    float* lufs_inst, int mem) {
+  if (!c || !x) return OMEGA_EINVAL;
+  if (mode < OMEGA_WEIGHT_K || mode > OMEGA_WEIGHT_Z) return fail(c, OMEGA_EINVAL, "weighting mode %d", mode);
+  // scipy's filtfilt needs more samples than its padlen (9 for the first section of K, A and C)
+  if (m < 1 || (mode != OMEGA_WEIGHT_Z && m <= 9))
+    return fail(c, OMEGA_EINVAL, "weighting: the length of the input (%d) must be greater than padlen (9)", m);
+  if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  HIPC(c, hipSetDevice(c->device));
+  std::vector<HostOut> outs;
+  const float* dx = x;
+  float* dw = weighted;
+  float* dl = lufs_inst;
+  int e = 0;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 0, x, (size_t)n * m * sizeof(float), reinterpret_cast<const void**>(&dx));
+    if (!e) e = stage_out(c, 5, weighted, (size_t)n * m, outs, &dw);
+    if (!e) e = stage_out(c, 2, lufs_inst, n, outs, &dl);
     if (e) return e;
-    KWeightParams kp{dx, m, 0, 1, n, tabs, nullptr, dl, dw, mode};
-    HIPC(c, launch_weight_ac(m, mode, kp, c->stream));
-  } else {
-    e = get_kw_tab(c, m, &tabs);
-    if (e) return e;
-    KWeightParams kp{dx, m, 0, 1, n, tabs, tabs + 1, dl, dw, mode};
-    HIPC(c, launch_kweight(m, kp, c->stream));
+  }
+  Weight64Params p{};
+  p.M = m;
+  p.mode = mode;
+  if (mode != OMEGA_WEIGHT_Z) {
+    if ((e = get_w64_stages(c, mode, &p.st))) return e;
+    p.n_st = mode == OMEGA_WEIGHT_A ? 4 : 2;
+  }
+  // float64 working buffers per frame: the signal and its odd extension (at most 64 MiB per launch)
+  p.scratch_stride = 2 * (int64_t)m + 32;
+  const int64_t per_launch = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)(8 << 20) / p.scratch_stride));
+  if (per_launch * p.scratch_stride > c->w64_cap) {
+    if ((e = dalloc(c, &c->d_w64, (size_t)(per_launch * p.scratch_stride)))) return e;
+    c->w64_cap = per_launch * p.scratch_stride;
+  }
+  p.scratch = c->d_w64;
+  for (int64_t f0 = 0; f0 < n; f0 += per_launch) {
+    p.x = dx + f0 * m;
+    p.n = std::min(per_launch, n - f0);
+    p.weighted_out = dw ? dw + f0 * m : nullptr;
+    p.lufs_out = dl ? dl + f0 : nullptr;
+    HIPC(c, launch_weight64(p, c->stream));
   }
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
@@ -1946,7 +2079,7 @@ int omega_chroma(omega_ctx* c, const float* spec, int64_t n, int32_t n_bins, dou
 
 int omega_rfft(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t window, float* mag, float* cplx, int mem) {
   if (!c || !x || (!mag && !cplx)) return OMEGA_EINVAL;
-  if (!is_pow2_in(m, 512, 16384)) return fail(c, OMEGA_EUNSUP, "rfft: length %d unsupported", m);
+  if (m < 1) return fail(c, OMEGA_EINVAL, "rfft: length %d", m);
   if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
   HIPC(c, hipSetDevice(c->device));
   float* win = nullptr;
@@ -1961,6 +2094,19 @@ int omega_rfft(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t windo
     if (!e) e = stage_out(c, 1, mag, (size_t)n * (m / 2 + 1), outs, &dm);
     if (!e) e = stage_out(c, 2, cplx, (size_t)n * (m / 2 + 1) * 2, outs, &dc);
     if (e) return e;
+  }
+  if (!is_pow2_in(m, 512, 16384)) {  // other lengths: the mixed-radix transform (anyfft.hip)
+    AnyFftParams ap{};
+    ap.x = dx;
+    ap.frame_stride = m;
+    ap.n = n;
+    ap.N = m;
+    ap.win = win;
+    ap.mag = dm;
+    ap.cplx = dc;
+    if ((e = run_any(c, ap, 0))) return e;
+    if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+    return 0;
   }
   RfftParams p{};
   p.x = dx;

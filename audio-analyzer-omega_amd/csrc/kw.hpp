@@ -372,58 +372,4 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
   OMEGA_STAMP(26);
 }
 
-// A- and C-weighting (professional_meters.py:74-127, :155-218): cascaded filtfilt stages on the
-// register-resident frame -- A: 2nd-order high-pass 20.6 Hz, 1st-order high-pass 107.7 Hz, 1st-order
-// low-pass 737.9 Hz, 2nd-order low-pass 12194 Hz, times 2.5 (:188); C: 2nd-order high-pass 20.6 Hz,
-// 2nd-order low-pass 12194 Hz -- with the same RMS gate and the instantaneous LUFS of the weighted
-// signal. tabs: the stages' scan tables (host, in order); pwl: LDS [4][kPwl].
-template <int M, int NTH, int MODE>
-__device__ __forceinline__ void weight_chain_body(const KWeightParams& p, const BiquadTab* __restrict__ tabs, int64_t cf,
-                                                  int tid, float4 (*pwl)[kPwl], float* sh, float* edge, double* red) {
-  constexpr int L = M / NTH;
-  constexpr int NS = MODE == 1 ? 4 : 2;
-  const int64_t f = cf / p.C, c = cf % p.C;
-  const float* __restrict__ x = p.x + f * p.frame_stride + c * p.chan_stride;
-  for (int i = tid; i < NS * kPwl; i += NTH) {
-    const BiquadTab& t = tabs[i / kPwl];
-    const int l = i % kPwl;
-    pwl[i / kPwl][l] = l < 64 ? make_float4(t.pw[l][0], t.pw[l][1], t.pw[l][2], t.pw[l][3])
-                              : make_float4(t.h0[l - 64], t.h1[l - 64], 0.f, 0.f);
-  }
-  float u[L];
-  static_for<0, L>([&](auto i) { u[i] = x[tid * L + i]; });
-  float ss = 0.f;
-  static_for<0, L>([&](auto i) { ss = fmaf(u[i], u[i], ss); });
-  const double ms_in = block_sum_f<NTH>(ss, red, tid) / M;
-  float* wout = p.weighted_out ? p.weighted_out + cf * M + tid * L : nullptr;
-  if (sqrt(ms_in) < 1e-6) {  // :158-160, :198-200
-    if (wout) static_for<0, L>([&](auto i) { wout[i] = 0.f; });
-    if (tid == 0 && p.lufs_out) p.lufs_out[cf] = -100.0f;
-    return;
-  }
-  auto stage = [&](auto si, auto E) {
-    gather_edges<L, NTH>(u, edge, tid);
-    __syncthreads();
-    filtfilt<L, NTH, 4, false, decltype(E)::value>(u, tabs + si, pwl[si], edge, sh, tid);
-    __syncthreads();  // the edges are read again by the next stage
-  };
-  using E9 = std::integral_constant<int, 9>;
-  using E6 = std::integral_constant<int, 6>;
-  if constexpr (MODE == 1) {
-    stage(std::integral_constant<int, 0>{}, E9{});
-    stage(std::integral_constant<int, 1>{}, E6{});
-    stage(std::integral_constant<int, 2>{}, E6{});
-    stage(std::integral_constant<int, 3>{}, E9{});
-    static_for<0, L>([&](auto i) { u[i] = u[i] * 2.5f; });  // filtered *= 2.5 (:188)
-  } else {
-    stage(std::integral_constant<int, 0>{}, E9{});
-    stage(std::integral_constant<int, 1>{}, E9{});
-  }
-  float acc = 0.f;
-  static_for<0, L>([&](auto i) { acc = fmaf(u[i], u[i], acc); });
-  if (wout) static_for<0, L>([&](auto i) { wout[i] = u[i]; });
-  const double ms = block_sum_f<NTH>(acc, red, tid) / M;
-  if (tid == 0 && p.lufs_out) p.lufs_out[cf] = ms > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms)) : -100.0f;
-}
-
 }  // namespace omega

@@ -51,39 +51,6 @@ __global__ __launch_bounds__(NTH, kw_waves_per_eu(NTH)) void kweight_kernel(KWei
   if constexpr (PUB) kw_count_in(p, threadIdx.x);
 }
 
-// A / C weighting: p.hp points at the mode's stage tables (4 for A, 2 for C)
-template <int M, int MODE, int NTH = kw_threads(M)>
-__global__ __launch_bounds__(NTH, kw_waves_per_eu(NTH)) void weight_ac_kernel(KWeightParams p) {
-  constexpr int NW = NTH / 64;
-  __shared__ float4 pwl[4][kPwl];
-  __shared__ float sh[4 * NW];
-  __shared__ float edge[20];
-  __shared__ double red[NW];
-  weight_chain_body<M, NTH, MODE>(p, p.hp, blockIdx.x, threadIdx.x, pwl, sh, edge, red);
-}
-
-hipError_t launch_weight_ac(int m, int mode, const KWeightParams& p, hipStream_t s) {
-  const dim3 grid((unsigned)p.n_cf);
-  switch (m) {
-#define OMEGA_AC(M)                                                                                        \
-  case M:                                                                                                  \
-    if (mode == 1)                                                                                         \
-      hipLaunchKernelGGL((weight_ac_kernel<M, 1>), grid, dim3(kw_threads(M)), 0, s, p);                   \
-    else                                                                                                   \
-      hipLaunchKernelGGL((weight_ac_kernel<M, 2>), grid, dim3(kw_threads(M)), 0, s, p);                   \
-    break;
-    OMEGA_AC(512)
-    OMEGA_AC(1024)
-    OMEGA_AC(2048)
-    OMEGA_AC(4096)
-    OMEGA_AC(8192)
-    OMEGA_AC(16384)
-#undef OMEGA_AC
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-
 OMEGA_STAMPS_GETTER(omega_debug_kw_stamps)
 
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s) {

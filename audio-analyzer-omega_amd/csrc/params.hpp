@@ -364,4 +364,46 @@ struct TransientParams {
   double* out;              // [n_frames, kTransientCols]
 };
 
+// omega_weighting (weight64.hip): scipy's float64 filtfilt cascades of professional_meters.py:129-218
+// for frames of any length > 9. One section: DF2T biquad (first-order sections have b2 = a2 = 0), its
+// lfilter_zi and filtfilt's padlen E.
+struct W64Stage {
+  double b0, b1, b2, a1, a2, zi0, zi1;
+  int E;
+  int pad_;
+};
+struct Weight64Params {
+  const float* x;           // [n, M]
+  int M;
+  int mode;                 // OMEGA_WEIGHT_K / A / C / Z
+  int64_t n;
+  W64Stage* st;             // the mode's sections in order
+  int n_st;
+  double* scratch;          // [n, scratch_stride]: signal (M) + odd extension (M + 2E)
+  int64_t scratch_stride;
+  float* weighted_out;      // [n, M] or nullptr
+  float* lufs_out;          // [n] or nullptr
+};
+
+// Frames of any length (anyfft.hip): mixed-radix Stockham transform, true peak and windowed rfft
+constexpr int kAnyMaxStages = 32;
+constexpr int kAnyLdsMax = 6826;  // 3 N float2 in 160 KiB of LDS; above: global scratch
+struct AnyFftParams {
+  const float* x;           // frame f at x + f * frame_stride
+  int64_t frame_stride;
+  int64_t n;
+  int N;
+  int n_stages;
+  int radix[kAnyMaxStages];
+  const float2* tw;         // [N] e^{-2 pi i m / N}
+  const float2* rot;        // [3 (N / 2) + 1] e^{2 pi i m / (4N)} (true peak)
+  float nyq_cos[4];         // cos(pi p / 4)
+  int phases;               // true peak: bit p set for each phase p in 1..3
+  float* tp_out;            // [n] dBTP
+  const float* win;         // rfft: window [N] or nullptr
+  float* mag;               // rfft: [n, N/2 + 1] or nullptr
+  float* cplx;              // rfft: [n, N/2 + 1, 2] or nullptr
+  float2* scratch;          // [n, 3N] when N > kAnyLdsMax, else nullptr (LDS)
+};
+
 }  // namespace omega

@@ -1,0 +1,173 @@
+// omega_weighting: ProfessionalMetering.apply_weighting + the instantaneous LUFS
+// (professional_meters.py:129-229, :236-246) at the reference's precision -- scipy's filtfilt runs
+// in float64 on the float32 frame -- for frames of any length above filtfilt's padlen.
+//
+//   gate   sqrt(mean(x^2)) < 1e-6 -> zeros                                    (:131-134, :158-160)
+//   K      f = filtfilt(hp38, x); s = filtfilt(shelf1500, f); y = f + (s - f) 0.3   (:137-151)
+//   A      four cascaded filtfilt sections, y *= 2.5                          (:162-190)
+//   C      two cascaded filtfilt sections                                     (:201-216)
+//   Z      y = x                                                              (:228-229)
+//   LUFS   -0.691 + 10 log10(mean(y^2)), -100 below 1e-10                     (:240-246)
+//
+// filtfilt per section (scipy 1.15.3 defaults): odd extension of E = 3 max(len(a), len(b)) samples
+// at each end (formed in float32 for the first section, whose input is the float32 frame, as scipy
+// forms it in the input dtype), DF2T lfilter forward from zi ext[0], backward from zi y[-1], crop.
+//
+// One 256-thread workgroup per frame, the float64 signal and its extension in a global working buffer
+// (L2-resident for a frame). Each lfilter pass is a chunked scan over the threads: every thread runs
+// its chunk of the 2-state recurrence s' = A s + B u from the zero state, the chunk carries are
+// combined by a Hillis-Steele scan in LDS with the powers P^(2^k) of P = A^L (computed per thread in
+// float64), and every thread re-runs its chunk from its true incoming state, writing the outputs.
+// The outputs come from the plain recurrence (y = b0 u + z0; z0 = b1 u + z1 - a1 y; z1 = b2 u - a2 y,
+// scipy's order), so they differ from scipy's sequential lfilter only by the rounding of the
+// incoming states (~1e-16 relative).
+#include <hip/hip_runtime.h>
+
+#include "params.hpp"
+
+namespace omega {
+
+constexpr int kW64Threads = 256;
+
+struct M2 {
+  double a, b, c, d;  // [[a, b], [c, d]]
+};
+__device__ __forceinline__ M2 mmul(const M2& x, const M2& y) {
+  return {x.a * y.a + x.b * y.c, x.a * y.b + x.b * y.d, x.c * y.a + x.d * y.c, x.c * y.b + x.d * y.d};
+}
+__device__ __forceinline__ double2 mvec(const M2& m, double2 v) {
+  return make_double2(m.a * v.x + m.b * v.y, m.c * v.x + m.d * v.y);
+}
+
+__device__ __forceinline__ double w64_block_sum(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// One lfilter pass over v[0..n) in place (rev: over v[n-1..0]), from the state s0.
+__device__ void w64_lfilter(double* v, int n, bool rev, const W64Stage& q, double2 s0, double2* sc) {
+  const int t = threadIdx.x;
+  const int L = (n + kW64Threads - 1) / kW64Threads;
+  const int lo = t * L, hi = min(lo + L, n);
+  auto at = [&](int k) -> double& { return v[rev ? n - 1 - k : k]; };
+  // 1) the chunk's end state from the zero state
+  double z0 = 0.0, z1 = 0.0;
+  for (int k = lo; k < hi; ++k) {
+    const double u = at(k);
+    const double y = q.b0 * u + z0;
+    z0 = q.b1 * u + z1 - q.a1 * y;
+    z1 = q.b2 * u - q.a2 * y;
+  }
+  // P = A^L, A = [[-a1, 1], [-a2, 0]]
+  const M2 A{-q.a1, 1.0, -q.a2, 0.0};
+  M2 P{1.0, 0.0, 0.0, 1.0}, Ak = A;
+  for (int e = L; e; e >>= 1) {
+    if (e & 1) P = mmul(P, Ak);
+    Ak = mmul(Ak, Ak);
+  }
+  double2 c = make_double2(z0, z1);
+  if (t == 0) c = make_double2(c.x + (P.a * s0.x + P.b * s0.y), c.y + (P.c * s0.x + P.d * s0.y));
+  // 2) inclusive scan of the carries: c_t = sum_j P^(t-j) e_j (the initial state folded into e_0)
+  M2 Pk = P;
+  for (int d = 1; d < kW64Threads; d <<= 1) {
+    sc[t] = c;
+    __syncthreads();
+    if (t >= d) {
+      const double2 o = mvec(Pk, sc[t - d]);
+      c = make_double2(c.x + o.x, c.y + o.y);
+    }
+    __syncthreads();
+    Pk = mmul(Pk, Pk);
+  }
+  sc[t] = c;
+  __syncthreads();
+  const double2 s = t == 0 ? s0 : sc[t - 1];
+  // 3) the chunk from its incoming state, outputs in place
+  z0 = s.x;
+  z1 = s.y;
+  for (int k = lo; k < hi; ++k) {
+    double& r = at(k);
+    const double u = r;
+    const double y = q.b0 * u + z0;
+    z0 = q.b1 * u + z1 - q.a1 * y;
+    z1 = q.b2 * u - q.a2 * y;
+    r = y;
+  }
+  __syncthreads();
+}
+
+// filtfilt of sig[0..M) (float64) with one section; out(k, value) consumes the cropped result
+template <class Out>
+__device__ void w64_filtfilt(const double* sig, bool f32_ext, double* ext, int M, const W64Stage& q, double2* sc,
+                             Out out) {
+  const int E = q.E, n = M + 2 * E;
+  const double x0 = sig[0], xl = sig[M - 1];
+  for (int j = threadIdx.x; j < n; j += kW64Threads) {
+    double v;
+    if (j >= E && j < E + M) {
+      v = sig[j - E];
+    } else {
+      const double a = j < E ? x0 : xl, b = j < E ? sig[E - j] : sig[M - 2 - (j - E - M)];
+      v = f32_ext ? (double)(2.0f * (float)a - (float)b) : 2.0 * a - b;  // odd_ext in the input dtype
+    }
+    ext[j] = v;
+  }
+  __syncthreads();
+  w64_lfilter(ext, n, false, q, make_double2(q.zi0 * ext[0], q.zi1 * ext[0]), sc);
+  w64_lfilter(ext, n, true, q, make_double2(q.zi0 * ext[n - 1], q.zi1 * ext[n - 1]), sc);
+  for (int k = threadIdx.x; k < M; k += kW64Threads) out(k, ext[E + k]);
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kW64Threads) void weight64_kernel(Weight64Params p) {
+  __shared__ double2 sc[kW64Threads];
+  __shared__ double red[4];
+  const int64_t f = blockIdx.x;
+  const int M = p.M;
+  const float* __restrict__ x = p.x + f * M;
+  double* sig = p.scratch + f * p.scratch_stride;
+  double* ext = sig + M;
+  double ss = 0.0;
+  for (int k = threadIdx.x; k < M; k += kW64Threads) {
+    const double v = x[k];
+    sig[k] = v;
+    ss += v * v;
+  }
+  const double ms_in = w64_block_sum(ss, red) / M;
+  float* wout = p.weighted_out ? p.weighted_out + f * M : nullptr;
+  if (p.mode != 3 && sqrt(ms_in) < 1e-6) {
+    if (wout)
+      for (int k = threadIdx.x; k < M; k += kW64Threads) wout[k] = 0.f;
+    if (threadIdx.x == 0 && p.lufs_out) p.lufs_out[f] = -100.0f;
+    return;
+  }
+  if (p.mode == 0) {  // K: f, then the 0.3 blend with the shelf-filtered f
+    w64_filtfilt(sig, true, ext, M, p.st[0], sc, [&](int k, double v) { sig[k] = v; });
+    w64_filtfilt(sig, false, ext, M, p.st[1], sc, [&](int k, double v) { sig[k] = sig[k] + (v - sig[k]) * 0.3; });
+  } else if (p.mode != 3) {
+    for (int s = 0; s < p.n_st; ++s) {
+      const double g = (p.mode == 1 && s == p.n_st - 1) ? 2.5 : 1.0;
+      w64_filtfilt(sig, s == 0, ext, M, p.st[s], sc, [&](int k, double v) { sig[k] = g == 1.0 ? v : v * g; });
+    }
+  }
+  double acc = 0.0;
+  for (int k = threadIdx.x; k < M; k += kW64Threads) {
+    const double v = sig[k];
+    acc += v * v;
+    if (wout) wout[k] = (float)v;
+  }
+  const double ms = w64_block_sum(acc, red) / M;
+  if (threadIdx.x == 0 && p.lufs_out) p.lufs_out[f] = ms > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms)) : -100.0f;
+}
+
+hipError_t launch_weight64(const Weight64Params& p, hipStream_t s) {
+  if (p.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(weight64_kernel, dim3((unsigned)p.n), dim3(kW64Threads), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace omega

@@ -13,8 +13,8 @@ The window is numpy's (np.hanning / np.hamming / else np.blackman, cast to float
 branch follows a float64 input's dtype; its CuPy branch casts to float32 like this one). The
 reference's result cache is kept as it is: keyed by (length, window, first 100 bytes of the input),
 ten entries, oldest evicted first (:103-111, :163-174) -- two inputs that share their first 100 bytes
-get the first one's spectrum, as in the reference. Sizes the device FFT does not run (powers of two
-512-16384) are logged and give zero spectra instead of raising (the reference never raises here).
+get the first one's spectrum, as in the reference. Every length runs on the device: powers of two
+512-16384 on the radix-16 / Stockham kernels, the others on the mixed-radix transform (anyfft.hip).
 """
 from __future__ import annotations
 
@@ -33,7 +33,7 @@ _SIZES = (512, 1024, 2048, 4096, 8192, 16384)
 
 
 def _supported(n: int) -> bool:
-    return n in _SIZES
+    return n >= 1
 
 
 class GPUAcceleratedFFT:
@@ -65,8 +65,7 @@ class GPUAcceleratedFFT:
                                      ("hann", "hamming") else "blackman", magnitude=True, complex_out=True)
             mag, cp = mag[0], cp[0]
         else:
-            logger.error("GPUAcceleratedFFT.compute_fft: length %d not supported on the device (powers of two "
-                         "512-16384)", n)
+            logger.error("GPUAcceleratedFFT.compute_fft: empty input")
             mag, cp = np.zeros(n // 2 + 1, np.float32), np.zeros(n // 2 + 1, np.complex64)
         with self.cache_lock:
             self.fft_cache[key] = {"magnitude": mag, "complex": cp if return_complex else None,

@@ -6,11 +6,13 @@ range / peak-hold deques all run on the MI355X (the deques live in the context a
 per-stream history). Filter coefficients are derived in the library (closed forms of
 scipy.signal.butter / lfilter_zi) and exposed here for inspection.
 
-Frames must be a power of two between 512 and 16384 samples: other lengths (the reference accepts
-any length > 9) are logged and leave the meters unchanged -- see DESIGN.md 'Scope'. Nothing here
-raises to the caller (the reference's convention): errors are logged and the previous values (or, for
-the weighted signal, zeros) returned. calculate_true_peak supports oversampling 1, 2 and 4 (the
-reference's default; 1 and 2 are phase subsets of the 4x polyphase transform).
+Frames of any length are metered, like the reference (its 4800-sample chunks included): the weighting
+runs scipy's float64 filtfilt cascade on the device (omega_weighting, any length above filtfilt's
+padlen of 9), the true peak the polyphase form of scipy's resample on the power-of-two kernels or, for
+other lengths, the mixed-radix transform (anyfft.hip). Nothing here raises to the caller (the
+reference's convention): errors (e.g. a frame of 9 samples or fewer, where scipy's filtfilt raises)
+are logged and the previous values (or, for the weighted signal, zeros) returned. calculate_true_peak
+supports oversampling 1, 2 and 4 (the reference's default; 1 and 2 are phase subsets of the 4x form).
 """
 from __future__ import annotations
 
@@ -20,12 +22,8 @@ from typing import Dict
 import numpy as np
 
 from .engine import Engine, Resolution
-from ._lib import UnsupportedError
 
 logger = logging.getLogger(__name__)
-
-_SUPPORTED = {512, 1024, 2048, 4096, 8192, 16384}
-
 
 def _butter2_highpass(fc: float, fs: float):
     k = np.tan(np.pi * fc / fs)
@@ -65,11 +63,9 @@ class ProfessionalMetering:
         self._eng = Engine([Resolution((20, 20000), 512, 256, 1.0)], sample_rate, min(20000, sample_rate / 2),
                            target_bins=2, frame_size=512, n_channels=1, device=device)
 
-    def _frame(self, audio_data):
-        x = np.asarray(audio_data, dtype=np.float32).ravel()
-        if len(x) not in _SUPPORTED:
-            raise UnsupportedError(-4, f"frame length {len(x)} not supported (power of two 512..16384)")
-        return x
+    @staticmethod
+    def _frame(audio_data):
+        return np.asarray(audio_data, dtype=np.float32).ravel()
 
     def apply_k_weighting(self, audio_data: np.ndarray) -> np.ndarray:
         """professional_meters.py:129-153 (returned as float64 like scipy's filtfilt)."""

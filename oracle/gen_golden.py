@@ -409,6 +409,46 @@ def gen_weighting_ac(R):
     np.savez_compressed(os.path.join(OUT, "weighting_ac.npz"), **d)
 
 
+def meters_any_seqs():
+    """Frames of lengths the power-of-two kernels do not take: the reference's own level-histogram and
+    peak-hold signals (test_enhanced_meters.py:82-135: 100 ms = 4800-sample float64 chunks), odd, prime
+    and 7-smooth lengths, and 200 ms frames (9600: above the LDS-resident transform size)."""
+    hist = []
+    for db in [-40, -30, -23, -20, -14, -10, -23, -23, -23]:
+        sig = 10 ** (db / 20) * np.sin(2 * np.pi * 1000 * np.linspace(0, 0.1, 4800))
+        hist += [sig] * 10
+    peaks = []
+    for db in [-6, -3, -1, -10]:
+        sig = np.zeros(4800)
+        sig[2400:2500] = 10 ** (db / 20)
+        peaks.append(sig)
+    rng = np.random.default_rng(17)
+    peaks += [0.001 * rng.standard_normal(4800) for _ in range(6)]
+    return {
+        "hist4800": np.stack(hist),
+        "peaks4800": np.stack(peaks),
+        "square480": np.stack([S.square(480)] * 3),
+        "noise1000": S.noise(21, 12 * 1000, 0.1).reshape(12, 1000),
+        "prime1021": (S.sine(440, 0.3, 6 * 1021) + S.noise(22, 6 * 1021, 0.02)).reshape(6, 1021),
+        "smooth4410": (S.sine(3000, 0.2, 5 * 4410) + S.noise(23, 5 * 4410, 0.05)).reshape(5, 4410),
+        "long9600": (S.sine(60, 0.5, 4 * 9600) + S.noise(24, 4 * 9600, 0.05)).reshape(4, 9600),
+        "tiny10": S.noise(25, 4 * 10, 0.3).reshape(4, 10),
+    }
+
+
+def gen_meters_any(R):
+    d = {"versions": VERSIONS}
+    for name, fr in meters_any_seqs().items():
+        li, tp, agg = _meter_run(R, fr)
+        d[f"{name}/x"] = fr
+        d[f"{name}/lufs_inst"], d[f"{name}/tp"], d[f"{name}/agg"] = li, tp, agg
+        pm = R.ProfessionalMetering(FS)
+        d[f"{name}/kw0"] = pm.apply_k_weighting(fr[0])
+        d[f"{name}/tp2"] = np.array([pm.calculate_true_peak(x, 2) for x in fr], np.float64)
+        d[f"{name}/tp1"] = np.array([pm.calculate_true_peak(x, 1) for x in fr], np.float64)
+    np.savez_compressed(os.path.join(OUT, "meters_any.npz"), **d)
+
+
 def gen_batched(R):
     d = {"versions": VERSIONS}
     bp = R.BatchedFFTProcessor()
@@ -574,6 +614,6 @@ if __name__ == "__main__":
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac"))]:
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac", "meters_any"))]:
         g(R)
         print("wrote", g.__name__)

@@ -132,6 +132,22 @@ def test_ac_weighting_lufs_sequence():
             assert abs(got[4] - g[f"seq/{mode}/agg"][f, 4]) < 1e-5  # float32 true peak (scipy's resample), 1 ulp
 
 
+@pytest.mark.parametrize("name", ["hist4800", "peaks4800", "square480", "noise1000", "prime1021", "smooth4410",
+                                  "long9600", "tiny10"])
+def test_meters_any_length_oracle(name):
+    """Frames of non-power-of-two lengths (the reference meters any chunk, test_enhanced_meters.py:82-135):
+    the oracle's LUFS_inst / true peak / aggregates against the reference's outputs."""
+    g = load_golden("meters_any")
+    fr = g[f"{name}/x"]
+    li, tp, agg = R.meter_sequence(fr, FS)
+    np.testing.assert_allclose(li, g[f"{name}/lufs_inst"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(tp, g[f"{name}/tp"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(agg[:, :4], g[f"{name}/agg"][:, :4], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(R.apply_k_weighting(fr[0], FS), g[f"{name}/kw0"], rtol=1e-12, atol=1e-14)
+    for o in (2, 1):
+        np.testing.assert_allclose([R.true_peak(x, o) for x in fr], g[f"{name}/tp{o}"], rtol=0, atol=1e-5)
+
+
 def test_filtfilt_restatement_matches_scipy():
     import scipy.signal as ss
     x = S.noise(3, 3000, 0.3).astype(np.float64)
