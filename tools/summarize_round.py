@@ -7,6 +7,8 @@
                               in-pipeline ones (overlapped with the other streams) and the roofline
                               probe's back-to-back ones (what bench.py's roofline.kernel_ms times)
   rNN_batch_traffic.json      HBM bytes per batch_kernel launch from FETCH_SIZE / WRITE_SIZE passes
+  rNN_cfg3_traffic.json       the same for the cfg3 spectra kernel (4096 x 8192-sample frames)
+  rNN_batch_pmc.txt / rNN_cfg3_pmc.txt  SQ counter groups per dispatch (VALU / LDS / wait cycles)
 
   python tools/summarize_round.py 01
 """
@@ -42,37 +44,62 @@ def main(rnd):
              "| kernel | dispatches | avg | min | max |", "|---|---|---|---|---|"]
     for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
         lines.append(f"| `{k}` | {len(v)} | {sum(v) / len(v):.1f} | {min(v):.1f} | {max(v):.1f} |")
-    tp = per.get(TP, [])
-    # bench.py: 55 pipeline steps (5 warmup + 50 timed) each launch one batch kernel, then the
-    # roofline probe launches it 3 + 20 times back to back, without the meter kernels beside it
+    # batch_kernel dispatches by grid: the cfg2 step's launch (512 channel-frames) comes first in bench.py --
+    # 55 pipeline steps (5 warmup + 50 timed), then the roofline probe's 3 + 20 back-to-back launches without
+    # the meter kernels beside it; cfg4 (8192 channel-frames per launch) and the cfg5 stream use other grids
+    bk = [r for r in rows if short(r["Kernel_Name"]) == TP]
     steps = 55
-    pipe, probe = tp[:steps], tp[steps:]
-    if probe:
-        timed = probe[3:]
-        lines += ["", f"Batch kernel `{TP}` (all per-channel-frame work of a step in one launch):", "",
+    if bk:
+        g0 = bk[0]["Grid_Size_X"]
+        cfg2 = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in bk if r["Grid_Size_X"] == g0]
+        pipe, timed = cfg2[:steps], cfg2[steps + 3:steps + 23]
+        lines += ["", f"Batch kernel `{TP}` (all per-channel-frame work of a step in one launch), cfg2 grid {g0}:", "",
                   f"- in the pipeline (the meter kernels run beside it on a side stream): {len(pipe)} dispatches, "
                   f"avg {sum(pipe) / len(pipe):.1f} us",
                   f"- roofline probe (alone, back to back; bench.py `roofline.kernel_ms` times these 20 with HIP "
-                  f"events): {len(timed)} dispatches, avg {sum(timed) / len(timed):.1f} us"]
+                  f"events): {len(timed)} dispatches, avg {sum(timed) / max(1, len(timed)):.1f} us"]
+        others = {}
+        for r in bk:
+            if r["Grid_Size_X"] != g0:
+                others.setdefault(r["Grid_Size_X"], []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        for gsz, v in others.items():
+            lines.append(f"- grid {gsz} (another bench leg: cfg4 launches 8192 channel-frames, the cfg5 stream and the ingest tests smaller batches): {len(v)} "
+                         f"dispatches, avg {sum(v) / len(v):.1f} us")
     b = json.loads([ln for ln in open(os.path.join(SRC, "stats.json")) if ln.startswith("{")][-1]) \
         if os.path.exists(os.path.join(SRC, "stats.json")) else json.load(open(os.path.join(SRC, "bench.json")))
     lines += ["", f"bench.py in the profiled run: roofline.kernel_ms = {b['roofline']['kernel_ms'] * 1e3:.1f} us, "
                   f"value = {b['value']:.0f} {b['unit']}, ms_per_step = {b['ms_per_step']:.4f}"]
     open(os.path.join(dst, f"r{rnd}_bench_dispatches.md"), "w").write("\n".join(lines) + "\n")
-    tr = {}
-    for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        f = glob.glob(os.path.join(SRC, f"pmc_{c}", "*counter_collection.csv"))[0]
-        v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if short(r["Kernel_Name"]) == TP]
-        tr[c] = sum(v) / len(v)
-        tr[c + "_dispatches"] = len(v)
-    out = {"kernel": TP, "command": "rocprofv3 --pmc {FETCH_SIZE|WRITE_SIZE} --kernel-trace -- python tools/kernel_bench.py batch --reps 20",
-           "fetch_size_kib": tr["FETCH_SIZE"], "write_size_kib": tr["WRITE_SIZE"],
-           "traffic_bytes": 2 * tr["FETCH_SIZE"] * 1024 + tr["WRITE_SIZE"] * 1024,
-           "dispatches": tr["FETCH_SIZE_dispatches"],
-           "method": "separate --pmc passes; FETCH_SIZE (KiB) doubled for gfx950 (MI355X_MICROARCH.md: it reports "
-                     "half the bytes of wide streaming reads), WRITE_SIZE (KiB) as reported",
-           "algorithmic_bytes": 512 * (16384 * 4 + 4 * (512 + 2))}
-    json.dump(out, open(os.path.join(dst, f"r{rnd}_batch_traffic.json"), "w"), indent=1)
+    for stage, kname, tag, alg, cmd in (
+            ("batch", TP, "batch", 512 * (16384 * 4 + 4 * (512 + 2)), "batch --reps 20"),
+            ("spectra", "spectra_rf_kernel", "cfg3", 4096 * (8192 * 4 + 4 * (512 + 12)), "spectra --reps 20")):
+        tr = {}
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(SRC, f"pmc_{stage}_{c}")
+            if not os.path.isdir(d):
+                d = os.path.join(SRC, f"pmc_{c}")  # round-1 layout (batch only)
+            f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+            v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if short(r["Kernel_Name"]).startswith(kname)]
+            tr[c] = sum(v) / len(v)
+            tr[c + "_dispatches"] = len(v)
+        out = {"kernel": kname, "command": f"rocprofv3 --pmc {{FETCH_SIZE|WRITE_SIZE}} --kernel-trace -- python tools/kernel_bench.py {cmd}",
+               "fetch_size_kib": tr["FETCH_SIZE"], "write_size_kib": tr["WRITE_SIZE"],
+               "traffic_bytes": 2 * tr["FETCH_SIZE"] * 1024 + tr["WRITE_SIZE"] * 1024,
+               "dispatches": tr["FETCH_SIZE_dispatches"],
+               "method": "separate --pmc passes; FETCH_SIZE (KiB) doubled for gfx950 (MI355X_MICROARCH.md: it reports "
+                         "half the bytes of wide streaming reads), WRITE_SIZE (KiB) as reported",
+               "algorithmic_bytes": alg}
+        json.dump(out, open(os.path.join(dst, f"r{rnd}_{tag}_traffic.json"), "w"), indent=1)
+        print(json.dumps(out, indent=1))
+        sq = os.path.join(SRC, f"sq_{stage}")
+        if os.path.isdir(sq):
+            import subprocess
+            txt = subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmcsum.py"), sq], capture_output=True,
+                                 text=True).stdout
+            hdr = (f"# rocprofv3 SQ counter groups (tools/profile_round.sh: one --pmc group per run, kernel-trace only) of\n"
+                   f"# python tools/kernel_bench.py {stage} --reps 5; per-dispatch averages (tools/pmcsum.py)\n")
+            open(os.path.join(dst, f"r{rnd}_{tag}_pmc.txt"), "w").write(hdr + txt)
+            print(txt)
     print(open(os.path.join(dst, f"r{rnd}_bench_dispatches.md")).read())
     print(json.dumps(out, indent=1))
 
