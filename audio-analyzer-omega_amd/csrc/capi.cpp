@@ -1366,7 +1366,7 @@ int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, cons
   if (n_bins < 1 || n_bins > kPostMaxBins || n_bands < 0 || n_bands > kPostMaxBands || !curve || !bass ||
       !comp_instr || !comp_vocal || !vocal_sup || !ranges || (n_bands && (!band_start || !band_end || !band_smooth)))
     return fail(c, OMEGA_EINVAL, "post configure: bad tables (n_bins %d, n_bands %d)", n_bins, n_bands);
-  if (p_lo < 0 || p_hi < p_lo || p_hi >= n_bins)
+  if (p_lo < 0 || p_hi < p_lo || p_hi > p_lo + 1 || p_hi >= n_bins)
     return fail(c, OMEGA_EINVAL, "post configure: percentile ranks %d, %d outside %d bins", p_lo, p_hi, n_bins);
   for (int b = 0; b < n_bands; ++b)
     if (band_start[b] < 0 || band_start[b] >= n_bins || band_end[b] > n_bins || band_end[b] < band_start[b])

@@ -45,10 +45,57 @@ __device__ __forceinline__ T block_reduce(T v, T* red, int t, Op op) {
 
 }  // namespace
 
+// order-preserving unsigned key of a float (-0 and +0 one key: numpy's sort holds them equal)
+__device__ __forceinline__ unsigned order_key(float v) {
+  const unsigned u = __float_as_uint(v == 0.f ? 0.f : v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// The value of sorted rank r of s[0..T) (no NaN): radix select over the order keys, 8 bits a round --
+// a histogram of the candidates' next digit (LDS atomics), the digit whose cumulative count passes r,
+// then the candidates narrowed to that digit. T / 256 elements per thread per round instead of the
+// T^2 / 256 comparisons of rank counting.
+__device__ float select_rank(const float* s, int T, int r, int t, unsigned* hist, unsigned* sel) {
+  unsigned prefix = 0, mask = 0;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[t] = 0;
+    __syncthreads();
+    for (int i = t; i < T; i += kPostThreads) {
+      const unsigned k = order_key(s[i]);
+      if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    // inclusive scan of the 256 counts: thread t owns digit t
+    const unsigned c = hist[t];
+    unsigned inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned u = __shfl_up(inc, o, 64);
+      if ((t & 63) >= o) inc += u;
+    }
+    if ((t & 63) == 63) sel[2 + (t >> 6)] = inc;
+    __syncthreads();
+    for (int w = 0; w < (t >> 6); ++w) inc += sel[2 + w];
+    const unsigned exc = inc - c;
+    if (c > 0 && exc <= (unsigned)r && (unsigned)r < inc) {
+      sel[0] = (unsigned)t;
+      sel[1] = (unsigned)r - exc;
+    }
+    __syncthreads();
+    prefix |= sel[0] << shift;
+    mask |= 255u << shift;
+    r = (int)sel[1];
+    __syncthreads();  // sel / hist reused by the next round
+  }
+  const unsigned u = (prefix & 0x80000000u) ? (prefix & 0x7FFFFFFFu) : ~prefix;
+  return __uint_as_float(u);
+}
+
 __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) {
   __shared__ float s[kPostMaxBins];
+  __shared__ unsigned hist[256];
+  __shared__ unsigned sel[2 + kPostThreads / 64];
   __shared__ float redf[kPostThreads / 64];
-  __shared__ float pv[2];
   const int t = threadIdx.x, T = p.T;
   const int64_t f = blockIdx.x;
   const float* in = p.in + f * p.stride;
@@ -101,20 +148,22 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
   // 3) 98th percentile (numpy 'linear', float32): the values of sorted ranks p_lo and p_hi
   // np.max and np.percentile propagate NaN: `nan > 0` is false, no normalisation
   if (mx > 0.f && !has_nan) {
-    if (t == 0) pv[0] = pv[1] = NAN;
-    __syncthreads();
+    const float a = select_rank(s, T, p.p_lo, t, hist, sel);
+    // rank p_hi (= p_lo or p_lo + 1): v_lo again while rank p_hi still holds a copy of it, else the
+    // smallest value above it
+    const unsigned klo = order_key(a);
+    int le = 0;
+    float above = INFINITY;
     for (int i = t; i < T; i += kPostThreads) {
       const float v = s[i];
-      int r = 0;
-      for (int j = 0; j < T; ++j) {
-        const float u = s[j];
-        r += (u < v) || (u == v && j < i);
-      }
-      if (r == p.p_lo) pv[0] = v;
-      if (r == p.p_hi) pv[1] = v;
+      if (order_key(v) <= klo)
+        ++le;
+      else
+        above = fminf(above, v);
     }
-    __syncthreads();
-    const float a = pv[0], b = pv[1], d = b - a;
+    le = block_reduce(le, reinterpret_cast<int*>(hist), t, [](int x, int y) { return x + y; });
+    above = block_reduce(above, redf, t, [](float x, float y) { return fminf(x, y); });
+    const float b = p.p_hi < le ? a : above, d = b - a;
     // numpy _lerp, no contraction
     const float ref = p.p_g >= 0.5f ? b - d * (1.0f - p.p_g) : a + d * p.p_g;
     if (ref > 0.f)
@@ -160,7 +209,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
 // Loads go in blocks of kEmaBlock frames (independent loads in flight; the recurrence is the only
 // dependence).
 constexpr int kEmaBlock = 32;
-constexpr int kEmaChunk = 128;
+constexpr int kEmaChunk = 64;
 constexpr int kEmaWarm = 256;
 __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
   const int b = blockIdx.x * 64 + threadIdx.x;
@@ -176,12 +225,20 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
   bool have = exact_start ? had : false;
   const float* col = p.band_raw + b;
   float* dst = p.band_out + b;
-  for (int64_t f0 = s0; f0 < c1; f0 += kEmaBlock) {
-    float v[kEmaBlock];
-    const int nf = c1 - f0 < kEmaBlock ? (int)(c1 - f0) : kEmaBlock;
+  // the next block's loads are issued before this block's recurrence (double-buffered registers)
+  float v[kEmaBlock], nx[kEmaBlock];
+  auto load = [&](float (&d)[kEmaBlock], int64_t g0) {
+    const int nf = c1 - g0 < kEmaBlock ? (int)(c1 - g0) : kEmaBlock;
 #pragma unroll
     for (int i = 0; i < kEmaBlock; ++i)
-      if (i < nf) v[i] = col[(f0 + i) * p.nb];
+      if (i < nf) d[i] = col[(g0 + i) * p.nb];
+  };
+  load(nx, s0);
+  for (int64_t f0 = s0; f0 < c1; f0 += kEmaBlock) {
+    const int nf = c1 - f0 < kEmaBlock ? (int)(c1 - f0) : kEmaBlock;
+#pragma unroll
+    for (int i = 0; i < kEmaBlock; ++i) v[i] = nx[i];
+    if (f0 + kEmaBlock < c1) load(nx, f0 + kEmaBlock);
 #pragma unroll
     for (int i = 0; i < kEmaBlock; ++i) {
       if (i < nf) {

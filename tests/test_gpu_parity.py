@@ -858,6 +858,30 @@ def test_app_post_nan_frame():
     np.testing.assert_array_equal(c, wc)
 
 
+def test_app_post_percentile_ties_and_zeros():
+    """The 98th percentile by radix select over the float order keys: spectra with heavy ties
+    (quantised values), runs of zeros (+0 and -0), negative values, a frame whose top 3 % are equal,
+    512- and 1024-bin frames, bitwise against the oracle (np.percentile)."""
+    from omega_gpu.app_post import SpectrumPostProcessor
+    rng = np.random.default_rng(13)
+    for T in (512, 1024):
+        freqs = np.linspace(0, 20000, T)
+        F = 12
+        x = (np.round(rng.random((F, T)) * 8) / 8).astype(np.float32)  # 9 distinct values
+        x[0, : T // 2] = 0.0
+        x[1, ::2] = -0.0
+        x[2] = np.float32(0.25)
+        x[2, -T // 32:] = np.float32(3.0)                                # top 3 % equal
+        x[3] = rng.standard_normal(T).astype(np.float32)                 # negative values
+        x[4, :-1] = 0.0
+        x[5] = np.arange(T, dtype=np.float32)[::-1]
+        pp = SpectrumPostProcessor(freqs, smoothing_enabled=False)
+        sp, b, c = pp.process(x)
+        ws, wb, wc = R.app_post_sequence(x, freqs, smoothing=False)
+        np.testing.assert_array_equal(sp, ws, err_msg=f"T={T}")
+        np.testing.assert_array_equal(c, wc)
+
+
 def test_app_post_random_state_and_device_input():
     """Random spectra (every content branch) against the oracle; calls of 1, 9 and the rest continue
     the band EMA; device input with a padded row stride; reset starts a new stream."""
