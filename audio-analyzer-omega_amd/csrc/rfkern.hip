@@ -255,6 +255,13 @@ hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s)
 // band and chroma tables are read from global memory, L1/L2-resident).
 constexpr int kSpecRfThreads = 256;
 constexpr int kSpecRfPeakWords = 12;  // peak bitmap of bins < 768: suppression reaches k / 2 < 1408 / 2
+// OMEGA_SPEC_PREFETCH: the band-table entries and the first chroma records loaded ahead of the
+// transform (1) or where they are used (0)
+#ifndef OMEGA_SPEC_PREFETCH
+#define OMEGA_SPEC_PREFETCH 1
+#endif
+constexpr bool kSpecPrefetch = OMEGA_SPEC_PREFETCH != 0;
+
 
 template <int K>
 __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraParams p) {
@@ -278,15 +285,50 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   const float2* __restrict__ twK = p.tw[ilog2(K)];
   const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];  // (issued before the frame: see truepeak_rf_body)
   const float2 wm = p.tw[ilog2(2 * K)][t];
+  // this thread's band-table entries (bands t, t + NTH) and chroma-group bounds, issued with the
+  // twiddles ahead of the frame: their latency is off the band / chroma phases' critical path
+  constexpr int kGrp = 20;  // chroma: threads per base-class group (12 x 20 = 240 of 256)
+  int bs[2] = {0, 0}, be[2] = {0, 0};
+  float bsc[2] = {1.f, 1.f};
+  static_for<0, 2>([&](auto j) {
+    const int i = t + NTH * j;
+    if (kSpecPrefetch && p.bands_out && i < p.n_valid) {
+      bs[j] = p.starts[i];
+      be[j] = p.ends[i];
+      if (p.scale) bsc[j] = p.scale[i];
+    }
+  });
+  int cj0 = 0, cj1 = 0;
+  if (kSpecPrefetch && p.chroma_out && t < 12 * kGrp) {
+    cj0 = p.cgoff[t / kGrp];
+    cj1 = p.cgoff[t / kGrp + 1];
+  }
   asm volatile("" ::: "memory");
+  OMEGA_STAMP_RT(30);
+  OMEGA_STAMP(0);
   static_for<0, 16>([&](auto r) {
     const float2 a = x2[t + NTH * r], w = w2[t + NTH * r];
     v[r] = make_float2(a.x * w.x, a.y * w.y);
   });
+  OMEGA_STAMP(1);
   FFT::template run<false, kRfTab>(v, buf, t, w1, w2b, p.rtw1, p.rtw2);
+  OMEGA_STAMP(2);
+  // the first two chroma records of this thread (group-ordered), issued now for the chroma phase
+  float4 ra0 = make_float4(0.f, 0.f, 0.f, 0.f), rb0 = ra0, ra1 = ra0, rb1 = ra0;
+  int cjf = cj0 + t % kGrp;
+  if (kSpecPrefetch && cjf < cj1) {
+    ra0 = p.crec[2 * cjf];
+    rb0 = p.crec[2 * cjf + 1];
+  }
+  if (kSpecPrefetch && cjf + kGrp < cj1) {
+    ra1 = p.crec[2 * (cjf + kGrp)];
+    rb1 = p.crec[2 * (cjf + kGrp) + 1];
+  }
+  asm volatile("" ::: "memory");
   __syncthreads();
   FFT::store_spectrum(v, buf, t);
   __syncthreads();
+  OMEGA_STAMP(3);
   float mg[16];
   float mnyq = 0.f, mx = 0.f;
   {
@@ -311,7 +353,9 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   __syncthreads();  // the untangle reads are done: the buffer becomes the magnitude array
   static_for<0, 16>([&](auto q) { magc[t + NTH * q] = mg[q]; });
   if (t == 0) magc[K] = mnyq;
+  OMEGA_STAMP(4);
   const float thr = block_max<NTH>(mx, redf, t) * 0.1f;  // np.max(fft) * 0.1 in float32 (barriers publish magc)
+  OMEGA_STAMP(5);
   if (p.mag_out) {
     float* o = p.mag_out + fr * (K + 1);
     static_for<0, 16>([&](auto q) { o[t + NTH * q] = mg[q]; });
@@ -319,7 +363,36 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   }
   if (p.bands_out) {
     float* o = p.bands_out + fr * p.n_out;
-    for (int i = t; i < p.n_out; i += NTH) {
+    auto band = [&](int i, int s, int e, float scale) {
+      float val = 0.f;
+      if (i < p.n_valid && s < K + 1 && e <= K + 1) {
+        float m0 = magc[s], m1 = m0, m2 = m0, m3 = m0;
+        int k = s + 1;
+        for (; k + 3 < e; k += 4) {
+          m0 = fmaxf(m0, magc[k]);
+          m1 = fmaxf(m1, magc[k + 1]);
+          m2 = fmaxf(m2, magc[k + 2]);
+          m3 = fmaxf(m3, magc[k + 3]);
+        }
+        for (; k < e; ++k) m0 = fmaxf(m0, magc[k]);
+        val = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3)) * scale;
+      }
+      o[i] = val;
+    };
+    static_for<0, 2>([&](auto j) {
+      const int i = t + NTH * j;
+      if (i < p.n_out) {
+        if constexpr (!kSpecPrefetch) {
+          if (i < p.n_valid) {
+            bs[j] = p.starts[i];
+            be[j] = p.ends[i];
+            if (p.scale) bsc[j] = p.scale[i];
+          }
+        }
+        band(i, bs[j], be[j], bsc[j]);
+      }
+    });
+    for (int i = t + 2 * NTH; i < p.n_out; i += NTH) {
       float val = 0.f;
       if (i < p.n_valid) {
         const int s = p.starts[i], e = p.ends[i];
@@ -339,6 +412,7 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
       o[i] = val;
     }
   }
+  OMEGA_STAMP(6);
   if (!p.chroma_out) return;
   // strict local maxima above 0.1 max (chromagram.py:166-170) among bins 1..K-1 below 768 (the only
   // ones a suppressed bin k / h, k < c_hi <= 1408, can name): bin t + NTH q is lane t % 64 of wave
@@ -358,6 +432,7 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
     });
   }
   __syncthreads();
+  OMEGA_STAMP(7);
   auto is_peak = [&](int q) { return q < 64 * kSpecRfPeakWords && (int)((pkw[q >> 6] >> (q & 63)) & 1ull); };
   // harmonic suppression (chromagram.py:172-187) as a scatter from the peaks, in the reference's
   // order per bin (h = 5, 4, 3, 2, float32 multiplies by float32(1/h)): round h scales bin q h of
@@ -374,11 +449,23 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
     });
     __syncthreads();
   });
-  constexpr int kGrp = 20;  // threads per base-class group (12 x 20 = 240 of 256)
+  OMEGA_STAMP(8);
   if (t < 12 * kGrp) {
     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    const int g = t / kGrp, r = t % kGrp;
-    const int j0 = p.cgoff[g], j1 = p.cgoff[g + 1];
+    if constexpr (!kSpecPrefetch) {
+      cj0 = p.cgoff[t / kGrp];
+      cj1 = p.cgoff[t / kGrp + 1];
+      cjf = cj0 + t % kGrp;
+      if (cjf < cj1) {
+        ra0 = p.crec[2 * cjf];
+        rb0 = p.crec[2 * cjf + 1];
+      }
+      if (cjf + kGrp < cj1) {
+        ra1 = p.crec[2 * (cjf + kGrp)];
+        rb1 = p.crec[2 * (cjf + kGrp) + 1];
+      }
+    }
+    const int j1 = cj1;
     // group-ordered 32-byte records (weights + bin): two records per iteration, all four loads of an
     // iteration independent (no permutation load in front of the weights)
     auto acc_rec = [&](const float4 a, const float4 b) {
@@ -389,7 +476,15 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
       acc[3] = fma(ed, (double)a.w, acc[3]);
       acc[4] = fma(ed, (double)b.x, acc[4]);
     };
-    int j = j0 + r;
+    int j = cjf;
+    if (j + kGrp < j1) {  // the prefetched pair
+      acc_rec(ra0, rb0);
+      acc_rec(ra1, rb1);
+      j += 2 * kGrp;
+    } else if (j < j1) {
+      acc_rec(ra0, rb0);
+      j += 2 * kGrp;
+    }
     for (; j + kGrp < j1; j += 2 * kGrp) {
       const float4 a0 = p.crec[2 * j], b0 = p.crec[2 * j + 1];
       const float4 a1 = p.crec[2 * (j + kGrp)], b1 = p.crec[2 * (j + kGrp) + 1];
@@ -400,7 +495,9 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
 #pragma unroll
     for (int o = 0; o < 5; ++o) part[t * 5 + o] = acc[o];
   }
+  OMEGA_STAMP(9);
   __syncthreads();
+  OMEGA_STAMP(10);
   if (t < 60) {  // group g, offset o -> class (g + o - 2) mod 12
     const int g = t / 5, o = t % 5;
     double sgo = 0.0;
@@ -420,6 +517,8 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
     for (int q = 0; q < 12; ++q) tot += __shfl(sm, q, 64);
     if (t < 12) p.chroma_out[fr * 12 + c] = tot > 0 ? sm / tot : sm;
   }
+  OMEGA_STAMP(11);
+  OMEGA_STAMP_RT(31);
 }
 
 hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s) {

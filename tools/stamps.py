@@ -26,8 +26,8 @@ def main(stage):
     li = torch.empty(512, device="cuda")
     getter = {"kw": "omega_debug_kw_stamps", "tp": "omega_debug_spectral_stamps", "tprf": "omega_debug_rf_stamps",
               "mrfft": "omega_debug_spectral_stamps", "meters": "omega_debug_meter_stamps",
-              "spectra": "omega_debug_spectra_stamps"}[stage]
-    if stage == "spectra":
+              "spectra": "omega_debug_spectra_stamps", "spectra_rf": "omega_debug_rf_stamps"}[stage]
+    if stage in ("spectra", "spectra_rf"):
         from omega_gpu import Resolution
         from omega_gpu.engine import BandTable
         x3 = torch.from_numpy(bench.cfg3_input(4096, 8192)).cuda()
@@ -44,7 +44,7 @@ def main(stage):
             eng._check(lib.omega_k_weighting(eng._ctx, x.data_ptr(), 512, 16384, None, li.data_ptr(), L.MEM_DEVICE))
         elif stage in ("tp", "tprf"):
             eng._check(lib.omega_true_peak(eng._ctx, x.data_ptr(), 512, 16384, li.data_ptr(), L.MEM_DEVICE))
-        elif stage == "spectra":
+        elif stage in ("spectra", "spectra_rf"):
             e3.spectra(x3, "hann", bands=bt, chroma=True)
         elif stage == "meters":
             eng._check(lib.omega_meter_update(eng._ctx, li.data_ptr(), tpv.data_ptr(), 256, met.data_ptr(),
@@ -54,19 +54,25 @@ def main(stage):
             eng.process_frames(x, 256, 2 * 16384, 16384, combined=True, lufs=False, true_peak=False,
                                out={"combined": comb})
     torch.cuda.synchronize()
-    buf = np.zeros(4 * 16 * 32, np.uint64)
+    buf = np.zeros(8 * 16 * 32, np.uint64)
     fn = getattr(lib, getter)
     fn.argtypes = [C.c_void_p]
     assert fn(buf.ctypes.data) == 0
-    st = buf.reshape(4, 16, 32).astype(np.int64)
-    for b in range(4):
-        base = st[b][st[b] > 0].min() if (st[b] > 0).any() else 0
-        print(f"workgroup {b}")
+    st = buf.reshape(8, 16, 32).astype(np.int64)
+    rt = st[:, :, 30:32]  # s_memrealtime (100 MHz) at the first / last point, when the kernel records it
+    t0 = rt[rt > 0].min() if (rt > 0).any() else 0
+    for b in range(8):
+        sub = st[b, :, :30]
+        base = sub[sub > 0].min() if (sub > 0).any() else 0
+        print(f"workgroup {'first' if b < 4 else 'last'} #{b % 4}")
         for w in range(16):
             row = st[b, w]
             if not (row > 0).any():
                 continue
-            print(f"  w{w:2d} " + " ".join(f"{s}:{int(v - base)}" for s, v in enumerate(row) if v > 0))
+            txt = " ".join(f"{s}:{int(v - base)}" for s, v in enumerate(row[:30]) if v > 0)
+            if (row[30:] > 0).any():
+                txt += f"  | realtime us: start {(row[30] - t0) / 100:.2f} end {(row[31] - t0) / 100:.2f}"
+            print(f"  w{w:2d} " + txt)
 
 
 if __name__ == "__main__":
