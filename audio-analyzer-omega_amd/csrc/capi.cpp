@@ -851,7 +851,9 @@ bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams&
 // first workgroup waits for that count, so `s` completes only after fork[0]'s work: no stream events
 // anywhere (each event record / wait cost ~7-13 us of idle GPU between kernels). cfg2 step on MI355X:
 // 79.5 us (order 3); 85.2 (2: K-weighting mixed with the true peaks), 110.4 (0: K-weighting as its own
-// kernel first: it mixes with nothing); the side-meter layout with events 99.2. Mixing the
+// kernel first: it mixes with nothing); 4 (the true peaks first, then K-weighting mixed with the
+// 16384-point resolution) the same as 3 within noise (81.2 vs 80.9 us per call); the side-meter
+// layout with events 99.2. Mixing the
 // latency-bound K-weighting scans with transform work is what pays (K-weighting alone 25.7 us, the
 // true peak 37, the resolutions 26.5; one batch launch of all three 73.9).
 int enqueue_batch(omega_ctx* c, const SpectralParams& sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
@@ -864,9 +866,15 @@ int enqueue_batch(omega_ctx* c, const SpectralParams& sp, KWeightParams kp, int 
   auto add = [&](int sg, int role, bool on) {
     if (on) seg[sg][ns[sg]++] = role;
   };
-  add(0, 0, kw_in_batch);
-  add(order == 1 || order == 2 ? 0 : 1, 1, do_tp);
-  add(order == 1 || order == 3 ? 0 : 1, 2, mr >= 0);
+  if (order == 4) {  // the true peaks first, then K-weighting mixed with the 16384-point resolution
+    add(0, 1, do_tp);
+    add(1, 0, kw_in_batch);
+    add(1, 2, mr >= 0);
+  } else {
+    add(0, 0, kw_in_batch);
+    add(order == 1 || order == 2 ? 0 : 1, 1, do_tp);
+    add(order == 1 || order == 3 ? 0 : 1, 2, mr >= 0);
+  }
   const int64_t groups = (n + 7) / 8;
   int64_t end = 0;
   for (int sg = 0; sg < 2; ++sg) {
