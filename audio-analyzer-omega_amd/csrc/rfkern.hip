@@ -14,6 +14,8 @@
 //     is the first pass's input, in registers; the forward FFT of Z' is conj(K * y_p) packed, reduced
 //     to max |.| from the last pass's registers.
 // Per frame: 4 transforms, 12 LDS exchanges of 64 KiB (the old 1024-thread radix-8 kernel: 19).
+#include <cstdlib>
+
 #include "stamps.hpp"
 
 namespace omega {
@@ -524,8 +526,12 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
 hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s) {
   // a suppressed bin k < c_hi names bin k / h >= k / 2, which must lie in the peak bitmap
   if (m != 8192 || (p.chroma_out && p.c_hi > 2 * 64 * kSpecRfPeakWords)) return hipErrorInvalidValue;
+  static const int pad = [] {  // development knob: extra dynamic LDS per workgroup (occupancy probe)
+    const char* e = std::getenv("OMEGA_SPEC_LDS_PAD");
+    return e ? std::atoi(e) : 0;
+  }();
   hipLaunchKernelGGL(spectra_rf_kernel<4096>, dim3((unsigned)p.n), dim3(kSpecRfThreads),
-                     (RegFFT<4096>::kSlots + 8) * sizeof(float2), s, p);
+                     (RegFFT<4096>::kSlots + 8) * sizeof(float2) + pad, s, p);
   return hipGetLastError();
 }
 
