@@ -455,8 +455,8 @@ int validate(omega_ctx* c, const omega_config* cfg) {
     return fail(c, OMEGA_EUNSUP, "frame_size %d: power of two 512..16384 required", cfg->frame_size);
   for (int r = 0; r < cfg->n_res; ++r) {
     const omega_resolution& q = cfg->res[r];
-    if (q.fft_size < 512 || q.fft_size > cfg->frame_size)
-      return fail(c, OMEGA_EUNSUP, "fft_size %d: 512..frame_size(%d) supported", q.fft_size, cfg->frame_size);
+    if (q.fft_size < 2 || q.fft_size > cfg->frame_size)
+      return fail(c, OMEGA_EUNSUP, "fft_size %d: 2..frame_size(%d) supported", q.fft_size, cfg->frame_size);
   }
   if (cfg->target_bins < 1 || cfg->target_bins > (1 << 24)) return fail(c, OMEGA_EINVAL, "target_bins out of range");
   if (cfg->n_channels < 1) return fail(c, OMEGA_EINVAL, "n_channels must be >= 1");

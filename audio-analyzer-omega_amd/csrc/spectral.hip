@@ -135,6 +135,53 @@ __global__ __launch_bounds__(256) void combine_kernel(CombineParams p) {
   }
 }
 
+// Resolutions of fewer than 512 points (FFTConfig allows any power of two, multi_resolution_fft.py:39):
+// one 64-thread workgroup per channel-frame, the windowed frame in LDS, each bin a direct sum over
+// the N <= 256 samples with the N-point twiddle table (float32, like numpy's single-precision rfft),
+// then the same epilogue as mrfft_frame (weighted magnitudes, combine entries).
+constexpr int kSmallThreads = 64;
+__global__ __launch_bounds__(kSmallThreads) void mrfft_small_kernel(SpectralParams p, int r) {
+  __shared__ float xs[256];
+  __shared__ float mag[129];
+  const ResParam& rp = p.res[r];
+  const int N = rp.n, K = N / 2, t = threadIdx.x;
+  const int64_t cf = blockIdx.x, f = cf / p.C, c = cf % p.C;
+  const float* __restrict__ x = p.x + f * p.frame_stride + c * p.chan_stride + rp.offset;
+  for (int n = t; n < N; n += kSmallThreads) xs[n] = x[n] * rp.win[n];
+  __syncthreads();
+  const float2* __restrict__ tw = p.tw[ilog2(N)];
+  for (int k = t; k <= K; k += kSmallThreads) {
+    float re = 0.f, im = 0.f;
+    int e = 0;
+    for (int n = 0; n < N; ++n) {
+      const float2 w = tw[e];
+      re = fmaf(xs[n], w.x, re);
+      im = fmaf(xs[n], w.y, im);
+      e = (e + k) & (N - 1);
+    }
+    mag[k] = sqrtf(re * re + im * im);
+  }
+  __syncthreads();
+  if (rp.mag_out) {
+    float* o = rp.mag_out + cf * (K + 1);
+    for (int k = t; k <= K; k += kSmallThreads) o[k] = mag[k] * rp.wgt[k];
+  }
+  if (p.comb_out) {
+    float* o = p.comb_out + cf * p.T;
+    for (int e = rp.ent_begin + t; e < rp.ent_end; e += kSmallThreads) {
+      const CombEnt en = p.ent[e];
+      const int tt = en.tm & 0xFFFFFF, op = en.tm >> 24;
+      const float v = fmaf(en.c1, mag[en.j + 1 <= K ? en.j + 1 : K], en.c0 * mag[en.j]);
+      if (op == 0)
+        o[tt] = v;
+      else if (op == 1)
+        o[tt] += v;
+      else
+        o[tt] = 0.f;
+    }
+  }
+}
+
 // ---- host launchers ----
 #define OMEGA_SWITCH_K(n, CALL) \
   switch (n) {                  \
@@ -155,6 +202,12 @@ hipError_t launch_mrfft_range(const SpectralParams& p, int r0, int r1, hipStream
   const dim3 grid((unsigned)p.n_cf);
   for (int r = r0; r < r1 && r < p.n_res; ++r) {
     if (!p.comb_out && !p.res[r].mag_out) continue;
+    if (p.res[r].n < 512) {
+      hipLaunchKernelGGL(mrfft_small_kernel, grid, dim3(kSmallThreads), 0, s, p, r);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      continue;
+    }
     if ((p.rf_sizes >> ilog2(p.res[r].n)) & 1) {
       const hipError_t e = launch_mrfft_rf(p.res[r].n, p, r, s);
       if (e != hipSuccess) return e;
@@ -209,7 +262,7 @@ hipError_t launch_mrfft_independent(const SpectralParams& p, hipStream_t s) {
   for (int r = 0; r < p.n_res; ++r) {
     if (!p.comb_out && !p.res[r].mag_out) continue;
     const int n = p.res[r].n;
-    if (n > 8192 || ((p.rf_sizes >> ilog2(n)) & 1)) {
+    if (n > 8192 || n < 512 || ((p.rf_sizes >> ilog2(n)) & 1)) {
       const hipError_t e = launch_mrfft_range(p, r, r + 1, s);
       if (e != hipSuccess) return e;
       continue;

@@ -409,6 +409,27 @@ def gen_weighting_ac(R):
     np.savez_compressed(os.path.join(OUT, "weighting_ac.npz"), **d)
 
 
+SMALL = [((20, 2000), 256, 128, 1.5), ((200, 6000), 128, 64, 1.2), ((1000, 12000), 64, 32, 1.0),
+         ((5000, 20000), 512, 256, 1.5)]
+
+
+def gen_mrfft_small(R):
+    """FFTConfig sizes below 512 (any power of two is valid, multi_resolution_fft.py:39): a fresh
+    MultiResolutionFFT per 512-sample frame, magnitudes and combine(512)."""
+    d = {"versions": VERSIONS}
+    frames = {"sine": S.sine(1000, 0.3, 512) + S.noise(31, 512, 0.01), "noise": S.noise(32, 512, 0.2),
+              "triad": S.triad(512)}
+    for name, x in frames.items():
+        m = _mrfft(R, SMALL)
+        res = m.process_audio_chunk(x)
+        d[f"{name}/x"] = x
+        d[f"{name}/res"] = np.array(sorted(res))
+        for i, fr in res.items():
+            d[f"{name}/mag{i}"] = fr.magnitude
+        d[f"{name}/comb512"] = m.combine_results_optimized(res, target_bins=512)[0]
+    np.savez_compressed(os.path.join(OUT, "mrfft_small.npz"), **d)
+
+
 def meters_any_seqs():
     """Frames of lengths the power-of-two kernels do not take: the reference's own level-histogram and
     peak-hold signals (test_enhanced_meters.py:82-135: 100 ms = 4800-sample float64 chunks), odd, prime
@@ -614,6 +635,6 @@ if __name__ == "__main__":
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac", "meters_any"))]:
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac", "meters_any", "mrfft_small"))]:
         g(R)
         print("wrote", g.__name__)

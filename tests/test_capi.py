@@ -86,7 +86,7 @@ def test_facade_constructor_errors():
 def test_unsupported_sizes_are_reported_not_faked():
     from omega_gpu import Engine, Resolution, UnsupportedError
     with pytest.raises(UnsupportedError):
-        Engine([Resolution((20, 200), 256, 128, 1.0)])  # below the 512-point kernels
+        Engine([Resolution((20, 200), 1024, 256, 1.0)], frame_size=256)  # frames below 512 samples
 
 
 def test_no_gpu_fails_loudly():

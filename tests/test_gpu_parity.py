@@ -84,6 +84,24 @@ def test_mrfft_golden_northstar(mr, k):
     assert normwise(c, mr[f"ns{k}/comb512"]) < SPEC_TOL
 
 
+SMALL = [((20, 2000), 256, 128, 1.5), ((200, 6000), 128, 64, 1.2), ((1000, 12000), 64, 32, 1.0),
+         ((5000, 20000), 512, 256, 1.5)]
+
+
+def test_mrfft_small_sizes_golden():
+    """Resolutions below 512 points (mrfft_small_kernel: direct sums over the N-point twiddle table)
+    mixed with a 512-point one, against the reference's MultiResolutionFFT."""
+    g = load_golden("mrfft_small")
+    for name in ("sine", "noise", "triad"):
+        m = _mrfft(SMALL)
+        res = m.process_audio_chunk(g[f"{name}/x"])
+        assert sorted(res) == list(g[f"{name}/res"])
+        for i, r in res.items():
+            assert normwise(r.magnitude, g[f"{name}/mag{i}"]) < SPEC_TOL, (name, i)
+        c, _ = m.combine_results_optimized(res, 512)
+        assert normwise(c, g[f"{name}/comb512"]) < SPEC_TOL
+
+
 def test_mrfft_stream_layout(mr):
     """One instance fed 512-sample chunks: CircularBuffer availability and contents."""
     m = _mrfft()

@@ -64,6 +64,20 @@ def test_mrfft_stream(mr):
         np.testing.assert_array_equal(r[i], mr[f"stream/mag{i}"])
 
 
+def test_mrfft_small_sizes_oracle():
+    """FFTConfig sizes below 512 (256 / 128 / 64 with 512): the oracle against the reference."""
+    g = load_golden("mrfft_small")
+    cfgs = [R.FFTConfig(*c) for c in ((((20, 2000), 256, 128, 1.5)), (((200, 6000), 128, 64, 1.2)),
+                                      (((1000, 12000), 64, 32, 1.0)), (((5000, 20000), 512, 256, 1.5)))]
+    for name in ("sine", "noise", "triad"):
+        res = R.mrfft_frame(g[f"{name}/x"], cfgs, FS)
+        assert sorted(res) == list(g[f"{name}/res"])
+        for i in res:
+            np.testing.assert_array_equal(res[i], g[f"{name}/mag{i}"])
+        c, _ = R.combine(res, cfgs, FS, 20000, 512)
+        np.testing.assert_allclose(c, g[f"{name}/comb512"], rtol=1e-6, atol=1e-7)
+
+
 def test_combine_plan_matches_combine(mr):
     """The host-side interpolation plan the HIP epilogue uses reproduces combine()."""
     x = mr["ns0/x"]
