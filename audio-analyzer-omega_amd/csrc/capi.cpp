@@ -282,7 +282,7 @@ struct omega_ctx {
   // transient-analysis tables per frame length: twiddles (float64) and the Savitzky-Golay weights
   std::map<int, std::pair<double2*, double2*>> tr_tw;
   double* d_sg = nullptr;
-  int64_t dflux_cap = 0;
+  int64_t dflux_cap = 0;  // (elements)
   // omega_weighting: float64 filter cascades per mode and the per-launch working buffers
   W64Stage* w64[4] = {};
   // frames of any length (anyfft.hip): per N the radices and the twiddle / rotation tables
@@ -342,6 +342,25 @@ int dalloc(omega_ctx* c, T** p, size_t count) {
   if (e != hipSuccess) return fail(c, OMEGA_ENOMEM, "hipMalloc(%zu): %s", count * sizeof(T), hipGetErrorString(e));
   c->allocs.push_back(q);
   *p = static_cast<T*>(q);
+  return 0;
+}
+
+// A per-call scratch buffer of at least `need` elements: grown by replacement (the old buffer freed
+// once the device is idle -- work already enqueued may still read it), so repeated calls with growing
+// sizes keep one buffer instead of accumulating them until omega_destroy.
+template <class T>
+int grow(omega_ctx* c, T** p, int64_t* cap, int64_t need) {
+  if (need <= *cap) return 0;
+  if (*p) {
+    HIPC(c, hipDeviceSynchronize());
+    auto it = std::find(c->allocs.begin(), c->allocs.end(), static_cast<void*>(*p));
+    if (it != c->allocs.end()) c->allocs.erase(it);
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+  }
+  if (int e = dalloc(c, p, (size_t)need)) return e;
+  *cap = need;
   return 0;
 }
 
@@ -1146,10 +1165,7 @@ int omega_vu_update(omega_ctx* c, const void* x, int32_t f64, int64_t n_updates,
     }
     if (int e = omega_vu_reset(c)) return e;
   }
-  if (n_updates * C > c->vu_ms_cap) {
-    if (int e = dalloc(c, &c->d_vu_ms, (size_t)n_updates * C)) return e;
-    c->vu_ms_cap = n_updates * C;
-  }
+  if (int e = grow(c, &c->d_vu_ms, &c->vu_ms_cap, n_updates * C)) return e;
   std::vector<HostOut> outs;
   const void* dx = x;
   const double* ddt = dt;
@@ -1315,11 +1331,7 @@ int omega_drum_features(omega_ctx* c, const float* mag, int64_t n_frames, int32_
     const int e = omega_drum_reset(c);
     if (e) return e;
   }
-  if (n_frames > c->dflux_cap) {
-    const int e = dalloc(c, &c->d_dflux, (size_t)n_frames * kDrumBands);
-    if (e) return e;
-    c->dflux_cap = n_frames;
-  }
+  if (int e = grow(c, &c->d_dflux, &c->dflux_cap, n_frames * kDrumBands)) return e;
   std::vector<HostOut> outs;
   const float* dm = mag;
   double* dout = out;
@@ -1454,10 +1466,8 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   p.spec_out = spectrum_out;
   p.band_out = bands_out;
   p.content_out = content_out;
-  if (c->post.nb && n_frames * c->post.nb > c->post_raw_cap) {
-    if (int e = dalloc(c, &c->d_post_raw, (size_t)n_frames * c->post.nb)) return e;
-    c->post_raw_cap = n_frames * c->post.nb;
-  }
+  if (c->post.nb)
+    if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, n_frames * c->post.nb)) return e;
   p.band_raw = c->d_post_raw;
   HIPC(c, launch_post(p, c->stream));
   return 0;
@@ -1752,10 +1762,7 @@ int run_any(omega_ctx* c, AnyFftParams p, int truepeak) {
   int64_t per = n;
   if (p.N > kAnyLdsMax) {
     per = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)(8 << 20) / (3 * (int64_t)p.N)));
-    if (per * 3 * p.N > c->any_cap) {
-      if (int e = dalloc(c, &c->d_any, (size_t)(per * 3 * p.N))) return e;
-      c->any_cap = per * 3 * p.N;
-    }
+    if (int e = grow(c, &c->d_any, &c->any_cap, per * 3 * p.N)) return e;
     p.scratch = c->d_any;
   }
   const int nb = p.N / 2 + 1;
@@ -1918,10 +1925,7 @@ int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t 
   // float64 working buffers per frame: the signal and its odd extension (at most 64 MiB per launch)
   p.scratch_stride = 2 * (int64_t)m + 32;
   const int64_t per_launch = std::max<int64_t>(1, std::min<int64_t>(n, (int64_t)(8 << 20) / p.scratch_stride));
-  if (per_launch * p.scratch_stride > c->w64_cap) {
-    if ((e = dalloc(c, &c->d_w64, (size_t)(per_launch * p.scratch_stride)))) return e;
-    c->w64_cap = per_launch * p.scratch_stride;
-  }
+  if ((e = grow(c, &c->d_w64, &c->w64_cap, per_launch * p.scratch_stride))) return e;
   p.scratch = c->d_w64;
   for (int64_t f0 = 0; f0 < n; f0 += per_launch) {
     p.x = dx + f0 * m;
