@@ -45,6 +45,7 @@ hipError_t launch_combine(const CombineParams& p, hipStream_t s);
 hipError_t launch_drum(const DrumParams& p, hipStream_t s);
 hipError_t launch_vu(const VuParams& p, hipStream_t s);
 hipError_t launch_transients(const TransientParams& p, hipStream_t s);
+hipError_t launch_transients_any(const TransientParams& p, hipStream_t s);
 hipError_t launch_post(const PostParams& p, hipStream_t s);
 hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s);
 }  // namespace omega
@@ -281,6 +282,9 @@ struct omega_ctx {
   int vu_cur = 0;
   // transient-analysis tables per frame length: twiddles (float64) and the Savitzky-Golay weights
   std::map<int, std::pair<double2*, double2*>> tr_tw;
+  std::map<int, std::pair<std::vector<int>, double2*>> tr_any;  // other lengths: radices, e^{-2 pi i m / n}
+  double2* d_tr_scratch = nullptr;
+  int64_t tr_scratch_cap = 0;
   double* d_sg = nullptr;
   int64_t dflux_cap = 0;  // (elements)
   // omega_weighting: float64 filter cascades per mode and the per-launch working buffers
@@ -1250,7 +1254,8 @@ int omega_transients(omega_ctx* c, const void* x, int32_t f64, int64_t n_frames,
                      double* out, int mem) {
   if (!c || !out) return OMEGA_EINVAL;
   if (!x || n_frames < 0 || frame_stride < n) return fail(c, OMEGA_EINVAL, "transients: bad frame layout");
-  if (n < 64 || n > 8192 || (n & (n - 1))) return fail(c, OMEGA_EUNSUP, "transients: frame length %d unsupported", n);
+  if (n < 64) return fail(c, OMEGA_EINVAL, "transients: frame length %d below 64 (transient.py:21)", n);
+  const bool pow2 = n <= 8192 && !(n & (n - 1));
   if (n_frames == 0) return 0;
   HIPC(c, hipSetDevice(c->device));
   if (!c->d_sg) {
@@ -1259,8 +1264,35 @@ int omega_transients(omega_ctx* c, const void* x, int32_t f64, int64_t n_frames,
     std::vector<double> v(&W[0][0], &W[0][0] + 21 * 21);
     if (int e = upload(c, &c->d_sg, v)) return e;
   }
-  auto it = c->tr_tw.find(n);
-  if (it == c->tr_tw.end()) {
+  TransientParams p{};
+  if (!pow2) {  // other lengths: the complex mixed-radix transform (transient_any_kernel)
+    auto ia = c->tr_any.find(n);
+    if (ia == c->tr_any.end()) {
+      std::vector<int> rad;
+      int r = n;
+      while (r % 4 == 0) rad.push_back(4), r /= 4;
+      for (int fct : {2, 3, 5, 7})
+        while (r % fct == 0) rad.push_back(fct), r /= fct;
+      for (int fct = 11; (int64_t)fct * fct <= r; fct += 2)
+        while (r % fct == 0) rad.push_back(fct), r /= fct;
+      if (r > 1) rad.push_back(r);
+      if ((int)rad.size() > kTrMaxStages) return fail(c, OMEGA_EUNSUP, "transients: length %d: too many factors", n);
+      std::vector<double2> tw(n);
+      for (int m = 0; m < n; ++m) tw[m] = make_double2(std::cos(2 * M_PI * m / n), -std::sin(2 * M_PI * m / n));
+      double2* d = nullptr;
+      if (int e = upload(c, &d, tw)) return e;
+      ia = c->tr_any.emplace(n, std::make_pair(rad, d)).first;
+    }
+    p.n_stages = (int)ia->second.first.size();
+    for (int i = 0; i < p.n_stages; ++i) p.radix[i] = ia->second.first[i];
+    p.twn = ia->second.second;
+    if ((size_t)n * 2 * sizeof(double2) > 160 * 1024 - 64) {  // global working buffers
+      if (int e = grow(c, &c->d_tr_scratch, &c->tr_scratch_cap, n_frames * 2 * (int64_t)n)) return e;
+      p.scratch = c->d_tr_scratch;
+    }
+  }
+  auto it = c->tr_tw.find(pow2 ? n : 0);
+  if (pow2 && it == c->tr_tw.end()) {
     const int K = n / 2;
     std::vector<double2> t1(K / 2 > 0 ? K / 2 : 1), t2(K + 1);
     for (int m = 0; m < K / 2; ++m) t1[m] = make_double2(std::cos(2 * M_PI * m / K), -std::sin(2 * M_PI * m / K));
@@ -1280,18 +1312,21 @@ int omega_transients(omega_ctx* c, const void* x, int32_t f64, int64_t n_frames,
     if (!e) e = stage_out(c, 1, out, (size_t)n_frames * kTransientCols, outs, &dout);
     if (e) return e;
   }
-  TransientParams p{};
   p.x = dx;
   p.f64 = f64 ? 1 : 0;
   p.n_frames = n_frames;
   p.n = n;
   p.frame_stride = frame_stride;
-  p.tw = it->second.first;
-  p.tw2 = it->second.second;
   p.sg = c->d_sg;
   p.fs = c->cfg.sample_rate;
   p.out = dout;
-  HIPC(c, launch_transients(p, c->stream));
+  if (pow2) {
+    p.tw = it->second.first;
+    p.tw2 = it->second.second;
+    HIPC(c, launch_transients(p, c->stream));
+  } else {
+    HIPC(c, launch_transients_any(p, c->stream));
+  }
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 }

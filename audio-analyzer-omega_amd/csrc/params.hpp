@@ -351,17 +351,24 @@ struct VuParams {
 
 // TransientAnalyzer.analyze_transients (transient.hip; transient.py:19-108), one frame per workgroup
 constexpr int kTransientCols = 6;  // detected, attack_time_ms, punch, envelope_peak, envelope_rms, envelope_mean
+constexpr int kTrMaxStages = 32;
 struct TransientParams {
   const void* x;
   int f64;
   int64_t n_frames;
-  int n;                    // frame length (power of two 64..8192)
+  int n;                    // frame length (>= 64; powers of two up to 8192 on the packed transform)
   int64_t frame_stride;
   const double2* tw;        // [n/4] e^{-2 pi i m / (n/2)}
   const double2* tw2;       // [n/2 + 1] e^{-2 pi i q / n}
   const double* sg;         // [21, 21] Savitzky-Golay (21, 3) weights by output position in the window
   double fs;
   double* out;              // [n_frames, kTransientCols]
+  // other lengths: a complex n-point mixed-radix transform (radices as anyfft.hip) with the float64
+  // table e^{-2 pi i m / n}, buffers in LDS (2 n double2) or, when scratch is set, global memory
+  int n_stages;
+  int radix[kTrMaxStages];
+  const double2* twn;       // [n] or nullptr (power-of-two path)
+  double2* scratch;         // [n_frames, 2 n] or nullptr
 };
 
 // omega_weighting (weight64.hip): scipy's float64 filtfilt cascades of professional_meters.py:129-218

@@ -258,7 +258,7 @@ int omega_vu_update(omega_ctx* ctx, const void* x, int32_t f64, int64_t n_update
 int omega_vu_reset(omega_ctx* ctx);
 
 /* TransientAnalyzer.analyze_transients (omega4/analyzers/transient.py:19-108) for n_frames frames of
- * n samples (power of two 64..8192; float32, or float64 when f64 != 0), frame f at x + f*frame_stride,
+ * n samples (any n >= 64, as the reference; float32, or float64 when f64 != 0), frame f at x + f*frame_stride,
  * in float64 like scipy: Hilbert envelope, Savitzky-Golay (21, 3) smoothing, attack points where the
  * envelope's derivative exceeds twice its standard deviation. out [n_frames, 6] float64:
  * transients_detected, attack_time (ms), punch_factor, envelope_peak, envelope_rms and the smoothed

@@ -470,6 +470,34 @@ def gen_meters_any(R):
     np.savez_compressed(os.path.join(OUT, "meters_any.npz"), **d)
 
 
+def gen_transients_any(R):
+    """analyze_transients on frames of lengths that are not powers of two (the reference takes any
+    length >= 64): 100 ms float64 chunks (4800), float32 1000 / 100, a prime (1021) and 9600 samples,
+    one analyzer per length group (its envelope history carries over)."""
+    d = {"versions": VERSIONS}
+    x64, x32 = transient_frames(seed=77)
+    rng = np.random.default_rng(78)
+    groups = {
+        "f64_4800": np.stack([np.resize(x64[k], 4800) * np.hanning(4800) for k in range(6)]),
+        "f32_1000": np.stack([x32[k][:1000] for k in range(5)]),
+        "f64_1021": np.stack([np.resize(x64[k], 1021) for k in range(4)]),
+        "f64_9600": np.stack([np.resize(x64[k], 9600) + 0.001 * rng.standard_normal(9600) for k in range(3)]),
+        "f32_100": np.stack([x32[k][:100] for k in range(4)]),
+        "zeros_3000": np.zeros((1, 3000)),
+    }
+    keys = ("transients_detected", "attack_time", "punch_factor", "envelope_peak", "envelope_rms")
+    for name, fr in groups.items():
+        ta = R.TransientAnalyzer(FS)
+        rec = []
+        for x in fr:
+            r = ta.analyze_transients(x)
+            rec.append([float(r.get(k, np.nan)) for k in keys])
+        d[f"{name}/x"] = fr
+        d[f"{name}/out"] = np.array(rec)
+        d[f"{name}/history"] = np.array(ta.get_envelope_history())
+    np.savez_compressed(os.path.join(OUT, "transients_any.npz"), **d)
+
+
 def gen_batched(R):
     d = {"versions": VERSIONS}
     bp = R.BatchedFFTProcessor()
@@ -635,6 +663,6 @@ if __name__ == "__main__":
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac", "meters_any", "mrfft_small"))]:
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac", "meters_any", "mrfft_small", "transients_any"))]:
         g(R)
         print("wrote", g.__name__)
