@@ -27,6 +27,13 @@
  *   omega_spectra          omega_rfft -> omega_bands_apply (MAX) + omega_chroma fused in one pass (cfg3)
  *   omega_drum_features    EnhancedKickDetector / EnhancedSnareDetector band flux, adaptive thresholds and
  *                          spectral centroid  omega4/analyzers/drum_detection.py:47-103, :212-305 (§8(f) row 1)
+ *   omega_weighting        ProfessionalMetering.apply_weighting (K / A / C / Z) professional_meters.py:74-229
+ *                          at scipy's float64 precision, any frame length above filtfilt's padlen
+ *   omega_post_*           the app's spectrum post-processing          omega4_main.py:748-1056 (§8(f) row 2)
+ *   omega_vu_*             VUMetersPanel.update ballistics             omega4/panels/vu_meters.py:55-99 (§8(f) row 2)
+ *   omega_ingest_*         capture chunks -> ring -> analysis          omega4/audio/capture.py:512-600,
+ *                          omega4_main.py:648-688 (§8(f) row 3)
+ *   omega_transients       TransientAnalyzer.analyze_transients        omega4/analyzers/transient.py:19-108 (§8(f) row 4)
  *
  * Conventions:
  *   - every function returns 0 on success and a negative omega_status on error; the message is
@@ -60,7 +67,8 @@ typedef enum {
   OMEGA_EINVAL = -1,  /* bad argument / config (the reference raises ValueError) */
   OMEGA_EHIP = -2,    /* HIP runtime error */
   OMEGA_ENOMEM = -3,
-  OMEGA_EUNSUP = -4   /* valid for the reference, not supported by this build (e.g. non power-of-2 M) */
+  OMEGA_EUNSUP = -4   /* valid for the reference, not supported by this build (e.g. a batch frame size W
+                         that is not a power of two 512..16384) */
 } omega_status;
 
 typedef enum { OMEGA_MEM_HOST = 0, OMEGA_MEM_DEVICE = 1 } omega_mem;
@@ -75,7 +83,7 @@ typedef enum {
 /* One FFT resolution: FFTConfig (multi_resolution_fft.py:26-44). */
 typedef struct {
   double freq_lo, freq_hi; /* inclusive range [lo, hi] in Hz */
-  int32_t fft_size;        /* power of two, 512..16384, <= frame_size */
+  int32_t fft_size;        /* power of two, 2..frame_size (below 512: mrfft_small_kernel) */
   int32_t hop_size;        /* kept for fidelity (CircularBuffer sizing); the frame API is stateless */
   double weight;           /* base psychoacoustic weight and combine weight */
   int32_t window;          /* omega_window */
