@@ -39,9 +39,16 @@ __device__ __forceinline__ float lane_xor1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
 
-template <int K>
+// TIGHT (K = 4096 only): the exchanges in exactly K slots (32 KiB, no padding) -- XOR swizzles
+// instead of padded rows, conflict-free as the padded layout (tools/model/regfft_model.py --tight):
+//   exchange 1  (t, k1)      -> 256 k1 + (t ^ 16 (k1 & 1))
+//   exchange 2  (u, k2, k1)  -> 256 k1 + 16 (k2 ^ (k1 & 1)) + (u ^ k2)   (per-access XOR addresses)
+//   spectrum    n            -> n ^ ((n >> 4) & 15)
+// so that a 256-thread workgroup's whole LDS fits 32 KiB (five per CU instead of four).
+template <int K, bool TIGHT = false>
 struct RegFFT {
   static_assert(K == 8192 || K == 4096, "register FFT plans: K = 4096, 8192");
+  static_assert(!TIGHT || K == 4096, "the tight layout is for K = 4096");
   static constexpr int NTH = K / 16;
   static constexpr int L = K / 256;
   // LDS layouts (float2 slots), padded so that every slot is a per-thread base plus a compile-time
@@ -52,26 +59,33 @@ struct RegFFT {
   static constexpr int P1 = L == 32 ? 512 : 272;
   static constexpr int P2R = L == 32 ? 544 : 272;
   static constexpr int P2C = L == 32 ? 34 : 17;
-  static constexpr int kSlots = K == 8192 ? 8712 : 4352;  // LDS buffer size in float2
+  static constexpr int kSlots = TIGHT ? 4096 : (K == 8192 ? 8712 : 4352);  // LDS buffer size in float2
 
   static __device__ __forceinline__ int a3(int n) {
-    if constexpr (K == 8192) return n + (n >> 4) + ((n >> 12) << 3);
+    if constexpr (TIGHT) return n ^ ((n >> 4) & 15);
+    else if constexpr (K == 8192) return n + (n >> 4) + ((n >> 12) << 3);
     else return n + (n >> 4);
   }
   // bins k = t + NTH r: a3(k) = s3(t) + o3(r)
-  static __device__ __forceinline__ int s3(int t) { return t + (t >> 4); }
-  static constexpr int o3(int r) { return K == 8192 ? 544 * r + 8 * (r >> 3) : 272 * r; }
-  // mirror bins K - t - NTH r, t >= 1: s3m(t) + o3(15 - r) (K = 8192, t = 0: exact except r = 0, 8)
-  static __device__ __forceinline__ int s3m(int t) { return (NTH - t) + ((NTH - t) >> 4); }
+  static __device__ __forceinline__ int s3(int t) {
+    if constexpr (TIGHT) return t ^ ((t >> 4) & 15);
+    else return t + (t >> 4);
+  }
+  static constexpr int o3(int r) { return TIGHT ? 256 * r : (K == 8192 ? 544 * r + 8 * (r >> 3) : 272 * r); }
+  // mirror bins K - t - NTH r, t >= 1: s3m(t) + o3(15 - r) (t = 0: exact except r = 0 (slot K: the
+  // callers' slack, or a guarded read under TIGHT) and, for K = 8192, r = 8)
+  static __device__ __forceinline__ int s3m(int t) { return s3(NTH - t); }
   // pass-3 output register m of thread s: frequency out_index(s, m), slot s3o(s) + 272 m
   static __device__ __forceinline__ int out_index(int s, int m) {
     if constexpr (L == 32) return (s >> 5) + 16 * ((s >> 1) & 15) + 256 * (m + 16 * (s & 1));
     else return (s >> 4) + 16 * (s & 15) + 256 * m;
   }
   static __device__ __forceinline__ int s3o(int s) {
-    if constexpr (L == 32) return (s >> 5) + 17 * ((s >> 1) & 15) + 4360 * (s & 1);
+    if constexpr (TIGHT) return ((s >> 4) ^ (s & 15)) + 16 * (s & 15);
+    else if constexpr (L == 32) return (s >> 5) + 17 * ((s >> 1) & 15) + 4360 * (s & 1);
     else return (s >> 4) + 17 * (s & 15);
   }
+  static constexpr int o3o(int m) { return TIGHT ? 256 * m : 272 * m; }
 
   // v[k] *= w^k, k = 1..15 (powers by a multiply chain)
   static __device__ __forceinline__ void twiddle(float2 (&v)[16], float2 w) {
@@ -122,7 +136,11 @@ struct RegFFT {
       twiddle(v, w1);
     }
     if constexpr (SYNC) __syncthreads();
-    {
+    if constexpr (TIGHT) {
+      float2* b0 = buf + t;
+      float2* b1 = buf + (t ^ 16);
+      static_for<0, 16>([&](auto k1) { (k1 & 1 ? b1 : b0)[256 * k1] = v[k1]; });
+    } else {
       float2* b = buf + t;
       static_for<0, 16>([&](auto k1) { b[P1 * k1] = v[k1]; });
     }
@@ -130,8 +148,15 @@ struct RegFFT {
     // pass 2
     {
       const int u = t % L, k1 = t / L;
-      const float2* b = buf + P1 * k1 + u;
-      static_for<0, 16>([&](auto r) { v[r] = b[L * r]; });
+      if constexpr (TIGHT) {  // element (u + 16 r, k1) at 256 k1 + u + 16 (r ^ (k1 & 1))
+        const int par = k1 & 1;
+        const float2* be = buf + 256 * k1 + u + 16 * par;
+        const float2* bo = buf + 256 * k1 + u - 16 * par;
+        static_for<0, 16>([&](auto r) { v[r] = (r & 1 ? bo : be)[16 * r]; });
+      } else {
+        const float2* b = buf + P1 * k1 + u;
+        static_for<0, 16>([&](auto r) { v[r] = b[L * r]; });
+      }
       if constexpr (TAB) {
         float4 q[8];
         load_tab(q, tw2 + u, L);
@@ -142,15 +167,27 @@ struct RegFFT {
         twiddle(v, w2);
       }
       __syncthreads();  // every exchange-1 read is done
-      float2* bw = buf + P2R * k1 + u;
-      static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
+      if constexpr (TIGHT) {  // (u, k2, k1) at 256 k1 + 16 (k2 ^ par) + (u ^ k2)
+        const int par = k1 & 1;
+        float2* be = buf + 256 * k1 + 16 * par;
+        float2* bo = buf + 256 * k1 - 16 * par;
+        static_for<0, 16>([&](auto k2) { (k2 & 1 ? bo : be)[16 * k2 + (u ^ k2)] = v[k2]; });
+      } else {
+        float2* bw = buf + P2R * k1 + u;
+        static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
+      }
     }
     __syncthreads();
     // pass 3
     if constexpr (L == 16) {
       const int k2 = t & 15, k1 = t >> 4;
-      const float2* b = buf + P2R * k1 + P2C * k2;
-      static_for<0, 16>([&](auto r) { v[r] = b[r]; });
+      if constexpr (TIGHT) {
+        const float2* b = buf + 256 * k1 + 16 * (k2 ^ (k1 & 1));
+        static_for<0, 16>([&](auto r) { v[r] = b[r ^ k2]; });
+      } else {
+        const float2* b = buf + P2R * k1 + P2C * k2;
+        static_for<0, 16>([&](auto r) { v[r] = b[r]; });
+      }
       dft16(v);
     } else {
       const int q = t & 1, k2 = (t >> 1) & 15, k1 = t >> 5;
@@ -171,7 +208,7 @@ struct RegFFT {
   // (the caller synchronises before, if the buffer may still be read, and after).
   static __device__ __forceinline__ void store_spectrum(const float2 (&v)[16], float2* buf, int t) {
     float2* b = buf + s3o(t);
-    static_for<0, 16>([&](auto m) { b[272 * m] = v[m]; });
+    static_for<0, 16>([&](auto m) { b[o3o(m)] = v[m]; });
   }
 };
 

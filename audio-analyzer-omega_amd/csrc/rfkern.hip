@@ -263,22 +263,35 @@ constexpr int kSpecRfPeakWords = 12;  // peak bitmap of bins < 768: suppression 
 #define OMEGA_SPEC_PREFETCH 1
 #endif
 constexpr bool kSpecPrefetch = OMEGA_SPEC_PREFETCH != 0;
+// OMEGA_SPEC_TIGHT: the cfg3 kernel's transform on the 32 KiB tight layout (RegFFT<4096, true>: five
+// workgroups per CU) or on the padded one (34.9 KiB: four)
+#ifndef OMEGA_SPEC_TIGHT
+#define OMEGA_SPEC_TIGHT 0
+#endif
+constexpr bool kSpecTight = OMEGA_SPEC_TIGHT != 0;
 
 
 template <int K>
 __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraParams p) {
-  using FFT = RegFFT<K>;
+  using FFT = RegFFT<K, kSpecTight>;
   constexpr int NTH = FFT::NTH;
   static_assert(NTH == kSpecRfThreads, "one 256-thread workgroup per frame");
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // the whole LDS of the workgroup is the exchange buffer (32 KiB with the tight layout: five
+  // workgroups per CU); after the transform it holds the magnitudes, the chroma partials, the peak
+  // bitmap and the reduction scratch
   float2* buf = reinterpret_cast<float2*>(smem);
   float* magc = reinterpret_cast<float*>(smem);  // |X_k|, k <= K, once the untangle is done
-  double* part = reinterpret_cast<double*>(smem + ((K + 1) * sizeof(float) + 15) / 16 * 16);  // [240][5]
-  static_assert(((K + 1) * sizeof(float) + 15) / 16 * 16 + 240 * 5 * sizeof(double) <= FFT::kSlots * sizeof(float2),
-                "chroma partials fit the exchange buffer");
-  __shared__ unsigned long long pkw[kSpecRfPeakWords];
-  __shared__ float redf[NTH / 64];
-  __shared__ double cls[12][5];
+  constexpr size_t kPartOff = ((K + 1) * sizeof(float) + 15) / 16 * 16;
+  constexpr size_t kPkwOff = kPartOff + 240 * 5 * sizeof(double);
+  constexpr size_t kClsOff = kPkwOff + kSpecRfPeakWords * sizeof(unsigned long long);
+  constexpr size_t kRedOff = kClsOff + 12 * 5 * sizeof(double);
+  static_assert(kRedOff + (NTH / 64) * sizeof(float) <= FFT::kSlots * sizeof(float2),
+                "magnitudes, chroma partials and scratch fit the exchange buffer");
+  double* part = reinterpret_cast<double*>(smem + kPartOff);  // [240][5]
+  unsigned long long* pkw = reinterpret_cast<unsigned long long*>(smem + kPkwOff);
+  double(*cls)[5] = reinterpret_cast<double(*)[5]>(smem + kClsOff);
+  float* redf = reinterpret_cast<float*>(smem + kRedOff);
   const int t = threadIdx.x;
   const int64_t fr = blockIdx.x;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + fr * p.stride);
@@ -338,7 +351,11 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
     const float2* bm = buf + FFT::s3m(t);
     static_for<0, 16>([&](auto q) {
       const float2 a = bo[FFT::o3(q)];
-      const float2 b = bm[FFT::o3(15 - q)];
+      float2 b;
+      if constexpr (kSpecTight && q == 0)
+        b = t == 0 ? a : bm[FFT::o3(15)];  // t = 0: slot K would lie past the tight buffer (value unused)
+      else
+        b = bm[FFT::o3(15 - q)];
       float2 xk, xkk;
       untangle(a, b, twc<q, 32>(wm), xk, xkk);
       mg[q] = cabs(xk);
@@ -530,8 +547,9 @@ hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s) {
     const char* e = std::getenv("OMEGA_SPEC_LDS_PAD");
     return e ? std::atoi(e) : 0;
   }();
-  hipLaunchKernelGGL(spectra_rf_kernel<4096>, dim3((unsigned)p.n), dim3(kSpecRfThreads),
-                     (RegFFT<4096>::kSlots + 8) * sizeof(float2) + pad, s, p);
+  using FFT = RegFFT<4096, kSpecTight>;
+  const size_t lds = FFT::kSlots * sizeof(float2) + (kSpecTight ? 0 : 8 * sizeof(float2)) + pad;
+  hipLaunchKernelGGL(spectra_rf_kernel<4096>, dim3((unsigned)p.n), dim3(kSpecRfThreads), lds, s, p);
   return hipGetLastError();
 }
 

@@ -135,6 +135,42 @@ class Plan:
         return worst
 
 
+class TightPlan4096(Plan):
+    """The tight K = 4096 layout (RegFFT<4096, true>): exactly K slots, XOR swizzles instead of padding."""
+
+    def __init__(self):
+        super().__init__(4096)
+
+    def a1(self, t, k1):
+        return 256 * k1 + (t ^ (16 * (k1 & 1)))
+
+    def a2(self, u, k2, k1):
+        return 256 * k1 + 16 * (k2 ^ (k1 & 1)) + (u ^ k2)
+
+    def a3(self, n):
+        return n ^ ((n >> 4) & 15)
+
+
+def check_tight():
+    pl = TightPlan4096()
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal(4096) + 1j * rng.standard_normal(4096)
+    err = np.max(np.abs(pl.fft(x) - np.fft.fft(x))) / np.max(np.abs(np.fft.fft(x)))
+    slots = [{pl.a1(t, k1) for t in range(256) for k1 in range(16)},
+             {pl.a2(u, k2, k1) for u in range(16) for k2 in range(16) for k1 in range(16)},
+             {pl.a3(n) for n in range(4096)}]
+    assert all(len(s) == 4096 and max(s) == 4095 for s in slots), "each exchange a bijection onto 4096 slots"
+    for t in range(256):  # the kernel's separable forms: base per thread + immediate offset per register
+        for r in range(16):
+            assert pl.a3(t + 256 * r) == (t ^ ((t >> 4) & 15)) + 256 * r
+            if t:
+                assert pl.a3(4096 - t - 256 * r) == ((256 - t) ^ (((256 - t) >> 4) & 15)) + 256 * (15 - r)
+    for s_ in range(256):
+        for m in range(16):
+            assert pl.a3(pl.out_index(s_, m)) == ((s_ >> 4) ^ (s_ & 15)) + 16 * (s_ & 15) + 256 * m
+    print(f"tight K=4096: fft err {err:.2e}, conflicts {pl.check_conflicts()}")
+
+
 def truepeak_model(x):
     """The kernel's true-peak flow: rfft via the packed K-point FFT, untangle per thread set
     S_t = {t + NTH r}, then per phase p = 1..3: Y_k = X_k rho_k^p (running product), mirror exchange,
@@ -168,6 +204,9 @@ def truepeak_model(x):
 
 
 def main():
+    if "--tight" in sys.argv:
+        check_tight()
+        return
     rng = np.random.default_rng(0)
     for K in (4096, 8192):
         pl = Plan(K)
