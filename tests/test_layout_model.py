@@ -1,0 +1,35 @@
+"""The register-FFT LDS layouts (csrc/regfft.hpp) as an index model (tools/model/regfft_model.py): each
+plan reproduces np.fft.fft, each exchange is a bijection onto its slots, and no exchange has LDS bank
+conflicts beyond the known 2-way natural-order reads -- for the padded K = 4096 / 8192 layouts and the tight
+32 KiB K = 4096 one (RegFFT<4096, true>)."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "model"))
+import regfft_model as M  # noqa: E402
+
+
+def _check(pl, n_slots_max, allowed=("x3m",)):
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(pl.K) + 1j * rng.standard_normal(pl.K)
+    ref = np.fft.fft(x)
+    assert np.max(np.abs(pl.fft(x) - ref)) / np.max(np.abs(ref)) < 1e-12
+    c = pl.check_conflicts()
+    assert all(v == 0 for k, v in c.items() if k not in allowed), c
+    assert all(c[k] <= 2 for k in allowed), c
+    s3 = {pl.a3(n) for n in range(pl.K)}
+    assert len(s3) == pl.K and max(s3) < n_slots_max
+
+
+def test_padded_layouts():
+    # (the padded natural-order spectrum reads cost one extra cycle on a few lane groups)
+    _check(M.Plan(4096), 4352, ("x3r", "x3m"))
+    _check(M.Plan(8192), 8712, ("x3r", "x3m"))
+
+
+def test_tight_layout():
+    pl = M.TightPlan4096()
+    _check(pl, 4096)
+    M.check_tight()
