@@ -379,6 +379,8 @@ struct W64Stage {
   int E;
   int pad_;
 };
+// weighting modes (omega.h omega_weighting_mode)
+enum WeightMode : int { kWeightK = 0, kWeightA = 1, kWeightC = 2, kWeightZ = 3 };
 struct Weight64Params {
   const float* x;           // [n, M]
   int M;

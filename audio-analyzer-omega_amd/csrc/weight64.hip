@@ -139,18 +139,18 @@ __global__ __launch_bounds__(kW64Threads) void weight64_kernel(Weight64Params p)
   }
   const double ms_in = w64_block_sum(ss, red) / M;
   float* wout = p.weighted_out ? p.weighted_out + f * M : nullptr;
-  if (p.mode != 3 && sqrt(ms_in) < 1e-6) {
+  if (p.mode != kWeightZ && sqrt(ms_in) < 1e-6) {
     if (wout)
       for (int k = threadIdx.x; k < M; k += kW64Threads) wout[k] = 0.f;
     if (threadIdx.x == 0 && p.lufs_out) p.lufs_out[f] = -100.0f;
     return;
   }
-  if (p.mode == 0) {  // K: f, then the 0.3 blend with the shelf-filtered f
+  if (p.mode == kWeightK) {  // K: f, then the 0.3 blend with the shelf-filtered f
     w64_filtfilt(sig, true, ext, M, p.st[0], sc, [&](int k, double v) { sig[k] = v; });
     w64_filtfilt(sig, false, ext, M, p.st[1], sc, [&](int k, double v) { sig[k] = sig[k] + (v - sig[k]) * 0.3; });
-  } else if (p.mode != 3) {
+  } else if (p.mode != kWeightZ) {  // A / C: the cascade
     for (int s = 0; s < p.n_st; ++s) {
-      const double g = (p.mode == 1 && s == p.n_st - 1) ? 2.5 : 1.0;
+      const double g = (p.mode == kWeightA && s == p.n_st - 1) ? 2.5 : 1.0;  // filtered *= 2.5 (:190)
       w64_filtfilt(sig, s == 0, ext, M, p.st[s], sc, [&](int k, double v) { sig[k] = g == 1.0 ? v : v * g; });
     }
   }
