@@ -1501,8 +1501,8 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   p.spec_out = spectrum_out;
   p.band_out = bands_out;
   p.content_out = content_out;
-  if (c->post.nb)
-    if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, n_frames * c->post.nb)) return e;
+  if (c->post.nb)  // (+ the EMA's spare rows: post.hip post_ema_kernel)
+    if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, (n_frames + kEmaSpareRows) * c->post.nb)) return e;
   p.band_raw = c->d_post_raw;
   HIPC(c, launch_post(p, c->stream));
   return 0;

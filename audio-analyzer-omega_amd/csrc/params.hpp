@@ -274,6 +274,7 @@ constexpr int kDrumCols = 14;
 
 // App spectrum post-processing (post.hip): per-bin tables from the host.
 constexpr int kPostMaxBins = 2048;
+constexpr int kEmaSpareRows = 32;  // band_raw rows past the last frame (post_ema_kernel's unguarded block loads)
 constexpr int kPostMaxBands = 1024;
 struct PostParams {
   const float* in;  // [n, stride] combined spectra

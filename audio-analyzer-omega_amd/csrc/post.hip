@@ -18,6 +18,12 @@
 // bin of that frame).
 //   post_frame_kernel: one 256-thread workgroup per frame (independent frames).
 //   post_ema_kernel: one thread per band, the frames in order (the EMA recurrence), loads in blocks.
+#include "stamps.hpp"
+
+namespace omega {
+OMEGA_STAMPS_DECL
+}  // namespace omega
+
 #include "fft.hpp"
 #include "numpy_emul.hpp"
 #include "params.hpp"
@@ -60,9 +66,31 @@ __device__ float select_rank(const float* s, int T, int r, int t, unsigned* hist
   for (int shift = 24; shift >= 0; shift -= 8) {
     hist[t] = 0;
     __syncthreads();
-    for (int i = t; i < T; i += kPostThreads) {
-      const unsigned k = order_key(s[i]);
-      if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+    // the top byte (sign and exponent) clusters in a few digits: there lanes with the same digit add
+    // once, by their first lane, instead of serialising on one LDS address; the later digits spread
+    // out and take plain atomics
+    for (int i0 = 0; i0 < T; i0 += kPostThreads) {
+      const int i = i0 + t;
+      unsigned d = 0;
+      bool want = false;
+      if (i < T) {
+        const unsigned k = order_key(s[i]);
+        want = (k & mask) == prefix;
+        d = (k >> shift) & 255u;
+      }
+      if (shift != 24) {
+        if (want) atomicAdd(&hist[d], 1u);
+        continue;
+      }
+      unsigned long long act = __ballot(want);
+      while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const unsigned ld = __shfl(d, leader, 64);
+        const unsigned long long peers = __ballot(want && d == ld);
+        if ((t & 63) == leader) atomicAdd(&hist[ld], (unsigned)__popcll(peers));
+        if (d == ld) want = false;
+        act &= ~peers;
+      }
     }
     __syncthreads();
     // inclusive scan of the 256 counts: thread t owns digit t
@@ -99,6 +127,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
   const int t = threadIdx.x, T = p.T;
   const int64_t f = blockIdx.x;
   const float* in = p.in + f * p.stride;
+  OMEGA_STAMP(0);
   // 1) equal-loudness curve (float64 product rounded into the float32 array) and bass boost
   for (int i = t; i < T; i += kPostThreads) {
     float v = in[i];
@@ -109,22 +138,22 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
     s[i] = v;
   }
   __syncthreads();
+  OMEGA_STAMP(1);
   // 2) content type from the range means (omega4_main.py:805-840; voice detection is not on the path):
-  // four np.mean calls, one thread each (waves 0-3); the max and a NaN flag by block reduction
+  // four np.mean calls, one wave each (wave w: range w), numpy's pairwise sum restated lane-parallel
+  // (numpy_emul.hpp: the leaf accumulators on 8 lanes each, the leaf sums combined in numpy's order)
   __shared__ float means[4];
+  __shared__ float leaves[4][64];
   __shared__ int anynan;
   if (t == 0) anynan = 0;
-  {
-    const int w = t >> 6;
-    if ((t & 63) == 0) {
-      float m = 0.f;
-      if (w == 0 && p.be < T) m = np_mean_f32(s, p.be);
-      if (w == 1 && p.ve < T) m = np_mean_f32(s + p.vs, p.ve - p.vs);
-      if (w == 2 && p.hs < T) m = np_mean_f32(s + p.hs, T - p.hs);
-      if (w == 3) m = np_mean_f32(s, T);
-      means[w] = m;
-    }
-  }
+  const int w = t >> 6;
+  int m_lo = 0, m_n = 0;
+  bool m_on = false;  // (an empty range gives numpy's NaN mean: 0 / 0)
+  if (w == 0 && p.be < T) m_on = true, m_n = p.be;
+  if (w == 1 && p.ve < T) m_on = true, m_lo = p.vs, m_n = p.ve - p.vs;
+  if (w == 2 && p.hs < T) m_on = true, m_lo = p.hs, m_n = T - p.hs;
+  if (w == 3) m_on = true, m_n = T;
+  if (m_on) np_leaf_sums_wave(s + m_lo, m_n, leaves[w]);
   auto fmx = [](float a, float b) { return fmaxf(a, b); };
   float mx = -INFINITY;
   bool nan_here = false;
@@ -134,8 +163,18 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
   }
   __syncthreads();  // anynan initialised
   if (nan_here) anynan = 1;
-  mx = block_reduce(mx, redf, t, fmx);  // (its barriers publish means[] and anynan)
+  mx = block_reduce(mx, redf, t, fmx);  // (its barriers publish the leaf sums and anynan)
+  if ((t & 63) == 0) {
+    float m = 0.f;
+    if (m_on) {
+      int idx = 0;
+      m = (float)((double)np_leaf_combine<6>(m_n, leaves[w], idx) / (double)m_n);
+    }
+    means[w] = m;
+  }
+  __syncthreads();
   const bool has_nan = anynan != 0;
+  OMEGA_STAMP(2);
   const float eb = means[0], ev = means[1], eh = means[2], et = means[3];
   int content = 0;  // 0 instrumental, 1 vocal, 2 bass-heavy
   if (et > 0.f) {  // (NaN means fail every comparison, as in numpy)
@@ -169,6 +208,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
     if (ref > 0.f)
       for (int i = t; i < T; i += kPostThreads) s[i] = s[i] / ref * 0.8f;
   }
+  OMEGA_STAMP(3);
   // 4) frequency compensation (factors by position) and 5) optional max normalisation
   const float* comp = p.comp[content == 1 ? 1 : 0];
   if (p.flags & 2)
@@ -182,6 +222,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
       for (int i = t; i < T; i += kPostThreads) s[i] = s[i] / m;
     __syncthreads();
   }
+  OMEGA_STAMP(4);
   for (int i = t; i < T; i += kPostThreads) p.spec_out[f * T + i] = s[i];
   // 6) band means -> sqrt -> clamp (before the EMA)
   for (int b = t; b < p.nb; b += kPostThreads) {
@@ -196,6 +237,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
     p.band_raw[f * p.nb + b] = v;
   }
   if (t == 0 && p.content_out) p.content_out[f] = content;
+  OMEGA_STAMP(5);
 }
 
 // band_raw holds the clamped band values of the n frames; the EMA runs over them in frame order into
@@ -209,6 +251,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
 // Loads go in blocks of kEmaBlock frames (independent loads in flight; the recurrence is the only
 // dependence).
 constexpr int kEmaBlock = 32;
+static_assert(kEmaBlock <= kEmaSpareRows, "the spare rows cover a block");
 constexpr int kEmaChunk = 64;
 constexpr int kEmaWarm = 256;
 __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
@@ -223,41 +266,64 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
   const bool exact_start = c0 == 0 || s0 == 0;
   float prev = (exact_start && had) ? p.prev[b] : 0.f;
   bool have = exact_start ? had : false;
-  const float* col = p.band_raw + b;
-  float* dst = p.band_out + b;
-  // the next block's loads are issued before this block's recurrence (double-buffered registers)
+  // the row stride in a VGPR (opaque): the per-frame offsets are then vector arithmetic, instead of
+  // 32 + 32 uniform 64-bit offsets the compiler would hold in (spilled) SGPRs
+  int nb = p.nb;
+  asm volatile("" : "+v"(nb));
+  // blocks of kEmaBlock frames from s0: c0 - s0 is a multiple of the block (kEmaWarm and kEmaChunk
+  // are), so a block is all warm-up or all output. Loads are never guarded: band_raw has kEmaBlock
+  // spare rows past the last frame (values never stored); only the stream's last partial block guards
+  // its stores. The next block's loads are issued before this block's recurrence (double-buffered).
   float v[kEmaBlock], nx[kEmaBlock];
   auto load = [&](float (&d)[kEmaBlock], int64_t g0) {
-    const int nf = c1 - g0 < kEmaBlock ? (int)(c1 - g0) : kEmaBlock;
+    const float* c = p.band_raw + g0 * nb + b;
 #pragma unroll
-    for (int i = 0; i < kEmaBlock; ++i)
-      if (i < nf) d[i] = col[(g0 + i) * p.nb];
+    for (int i = 0; i < kEmaBlock; ++i) {
+      d[i] = *c;
+      c += nb;
+    }
   };
   load(nx, s0);
   for (int64_t f0 = s0; f0 < c1; f0 += kEmaBlock) {
-    const int nf = c1 - f0 < kEmaBlock ? (int)(c1 - f0) : kEmaBlock;
 #pragma unroll
     for (int i = 0; i < kEmaBlock; ++i) v[i] = nx[i];
     if (f0 + kEmaBlock < c1) load(nx, f0 + kEmaBlock);
+    if (smooth) {
+      // frame 0 of the block: no previous value only at a stream's very start
+      if (have) v[0] = prev * sf + v[0] * sf1;
 #pragma unroll
-    for (int i = 0; i < kEmaBlock; ++i) {
-      if (i < nf) {
-        if (smooth && have) v[i] = prev * sf + v[i] * sf1;
-        prev = v[i];
-        have = true;
-      }
+      for (int i = 1; i < kEmaBlock; ++i) v[i] = v[i - 1] * sf + v[i] * sf1;
     }
-    // only this chunk's frames are written (the warm-up frames belong to the chunk before)
-    if (f0 + kEmaBlock > c0) {
+    have = true;
+    const int nf = c1 - f0 < kEmaBlock ? (int)(c1 - f0) : kEmaBlock;
+    prev = v[kEmaBlock - 1];
+    if (nf < kEmaBlock) {
 #pragma unroll
-      for (int i = 0; i < kEmaBlock; ++i)
-        if (i < nf && f0 + i >= c0) dst[(f0 + i) * p.nb] = v[i];
+      for (int i = 0; i < kEmaBlock - 1; ++i) prev = i == nf - 1 ? v[i] : prev;
+    }
+    if (f0 >= c0) {  // this chunk's frames (the warm-up frames belong to the chunk before)
+      float* o = p.band_out + f0 * nb + b;
+      if (nf == kEmaBlock) {
+#pragma unroll
+        for (int i = 0; i < kEmaBlock; ++i) {
+          *o = v[i];
+          o += nb;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kEmaBlock; ++i) {
+          if (i < nf) *o = v[i];
+          o += nb;
+        }
+      }
     }
   }
   if (c1 == p.n) p.prev[b] = prev;
 }
 
 __global__ void post_flag_kernel(int* has_prev) { *has_prev = 1; }
+
+OMEGA_STAMPS_GETTER(omega_debug_post_stamps)
 
 hipError_t launch_post(const PostParams& p, hipStream_t s) {
   if (p.T < 1 || p.T > kPostMaxBins || p.nb < 0 || p.nb > kPostMaxBands) return hipErrorInvalidValue;

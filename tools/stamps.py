@@ -26,7 +26,8 @@ def main(stage):
     li = torch.empty(512, device="cuda")
     getter = {"kw": "omega_debug_kw_stamps", "tp": "omega_debug_spectral_stamps", "tprf": "omega_debug_rf_stamps",
               "mrfft": "omega_debug_spectral_stamps", "meters": "omega_debug_meter_stamps",
-              "spectra": "omega_debug_spectra_stamps", "spectra_rf": "omega_debug_rf_stamps"}[stage]
+              "spectra": "omega_debug_spectra_stamps", "spectra_rf": "omega_debug_rf_stamps",
+              "post": "omega_debug_post_stamps"}[stage]
     if stage in ("spectra", "spectra_rf"):
         from omega_gpu import Resolution
         from omega_gpu.engine import BandTable
@@ -46,6 +47,12 @@ def main(stage):
             eng._check(lib.omega_true_peak(eng._ctx, x.data_ptr(), 512, 16384, li.data_ptr(), L.MEM_DEVICE))
         elif stage in ("spectra", "spectra_rf"):
             e3.spectra(x3, "hann", bands=bt, chroma=True)
+        elif stage == "post":
+            if "pp" not in locals():
+                from omega_gpu.app_post import SpectrumPostProcessor
+                pp = SpectrumPostProcessor(np.linspace(20, 20000, 512))
+                xp = torch.from_numpy(np.random.default_rng(6).random((4096, 512)).astype(np.float32)).cuda()
+            pp.process(xp)
         elif stage == "meters":
             eng._check(lib.omega_meter_update(eng._ctx, li.data_ptr(), tpv.data_ptr(), 256, met.data_ptr(),
                                               L.MEM_DEVICE))
