@@ -61,11 +61,15 @@ __device__ __forceinline__ unsigned order_key(float v) {
 // a histogram of the candidates' next digit (LDS atomics), the digit whose cumulative count passes r,
 // then the candidates narrowed to that digit. T / 256 elements per thread per round instead of the
 // T^2 / 256 comparisons of rank counting.
-__device__ float select_rank(const float* s, int T, int r, int t, unsigned* hist, unsigned* sel) {
+__device__ float select_rank(const float* s, int T, int r, int t, unsigned (*hist)[256], unsigned (*sel)[8]) {
+  // histograms and selection words double-buffered by round parity: each round clears the next
+  // round's histogram while it scans its own, so a round needs three barriers
   unsigned prefix = 0, mask = 0;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    hist[t] = 0;
-    __syncthreads();
+  hist[0][t] = 0;
+  __syncthreads();
+  for (int round = 0, shift = 24; shift >= 0; ++round, shift -= 8) {
+    unsigned* h = hist[round & 1];
+    unsigned* sl = sel[round & 1];
     // the top byte (sign and exponent) clusters in a few digits: there lanes with the same digit add
     // once, by their first lane, instead of serialising on one LDS address; the later digits spread
     // out and take plain atomics
@@ -79,7 +83,7 @@ __device__ float select_rank(const float* s, int T, int r, int t, unsigned* hist
         d = (k >> shift) & 255u;
       }
       if (shift != 24) {
-        if (want) atomicAdd(&hist[d], 1u);
+        if (want) atomicAdd(&h[d], 1u);
         continue;
       }
       unsigned long long act = __ballot(want);
@@ -87,33 +91,33 @@ __device__ float select_rank(const float* s, int T, int r, int t, unsigned* hist
         const int leader = __ffsll((long long)act) - 1;
         const unsigned ld = __shfl(d, leader, 64);
         const unsigned long long peers = __ballot(want && d == ld);
-        if ((t & 63) == leader) atomicAdd(&hist[ld], (unsigned)__popcll(peers));
+        if ((t & 63) == leader) atomicAdd(&h[ld], (unsigned)__popcll(peers));
         if (d == ld) want = false;
         act &= ~peers;
       }
     }
     __syncthreads();
     // inclusive scan of the 256 counts: thread t owns digit t
-    const unsigned c = hist[t];
+    const unsigned c = h[t];
     unsigned inc = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const unsigned u = __shfl_up(inc, o, 64);
       if ((t & 63) >= o) inc += u;
     }
-    if ((t & 63) == 63) sel[2 + (t >> 6)] = inc;
+    if ((t & 63) == 63) sl[2 + (t >> 6)] = inc;
+    hist[(round + 1) & 1][t] = 0;
     __syncthreads();
-    for (int w = 0; w < (t >> 6); ++w) inc += sel[2 + w];
+    for (int w = 0; w < (t >> 6); ++w) inc += sl[2 + w];
     const unsigned exc = inc - c;
     if (c > 0 && exc <= (unsigned)r && (unsigned)r < inc) {
-      sel[0] = (unsigned)t;
-      sel[1] = (unsigned)r - exc;
+      sl[0] = (unsigned)t;
+      sl[1] = (unsigned)r - exc;
     }
     __syncthreads();
-    prefix |= sel[0] << shift;
+    prefix |= sl[0] << shift;
     mask |= 255u << shift;
-    r = (int)sel[1];
-    __syncthreads();  // sel / hist reused by the next round
+    r = (int)sl[1];
   }
   const unsigned u = (prefix & 0x80000000u) ? (prefix & 0x7FFFFFFFu) : ~prefix;
   return __uint_as_float(u);
@@ -121,8 +125,8 @@ __device__ float select_rank(const float* s, int T, int r, int t, unsigned* hist
 
 __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) {
   __shared__ float s[kPostMaxBins];
-  __shared__ unsigned hist[256];
-  __shared__ unsigned sel[2 + kPostThreads / 64];
+  __shared__ unsigned hist[2][256];
+  __shared__ unsigned sel[2][8];
   __shared__ float redf[kPostThreads / 64];
   const int t = threadIdx.x, T = p.T;
   const int64_t f = blockIdx.x;
