@@ -1458,9 +1458,11 @@ int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, cons
   if (!e) e = up(&dbs, band_start, (size_t)n_bands);
   if (!e) e = up(&dbe, band_end, (size_t)n_bands);
   if (!e) e = up(&dsf, band_smooth, (size_t)n_bands * 2);
-  if (!e) e = dalloc(c, &p.prev, (size_t)std::max(n_bands, 1));
-  if (!e) e = dalloc(c, &p.has_prev, 1);
+  if (!e) e = dalloc(c, &p.prev, (size_t)std::max(n_bands, 1) * 2);  // two EMA state buffers
+  if (!e) e = dalloc(c, &p.has_prev, 2);
   if (e) return e;
+  p.prev_out = p.prev + std::max(n_bands, 1);
+  p.has_prev_out = p.has_prev + 1;
   p.curve = dc;
   p.bass = db;
   p.comp[0] = d0;
@@ -1477,7 +1479,7 @@ int omega_post_reset(omega_ctx* c) {
   if (!c) return OMEGA_EINVAL;
   if (!c->post.T) return 0;
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMemsetAsync(c->post.has_prev, 0, sizeof(int), c->stream));
+  HIPC(c, hipMemsetAsync(std::min(c->post.has_prev, c->post.has_prev_out), 0, 2 * sizeof(int), c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -1505,6 +1507,10 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
     if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, (n_frames + kEmaSpareRows) * c->post.nb)) return e;
   p.band_raw = c->d_post_raw;
   HIPC(c, launch_post(p, c->stream));
+  if (c->post.nb) {  // the EMA wrote the other state buffer: it is the next call's input
+    std::swap(c->post.prev, c->post.prev_out);
+    std::swap(c->post.has_prev, c->post.has_prev_out);
+  }
   return 0;
 }
 

@@ -297,8 +297,10 @@ struct PostParams {
   float* band_out;             // [n, nb]
   float* band_raw;             // [n, nb] scratch: the clamped band values before the EMA
   int* content_out;            // [n]
-  float* prev;                 // [nb] EMA state
+  float* prev;                 // [nb] EMA state in (double-buffered: the kernels read one, write the other)
   int* has_prev;
+  float* prev_out;             // [nb] EMA state out
+  int* has_prev_out;
 };
 
 struct DrumParams {

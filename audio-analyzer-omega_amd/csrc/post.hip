@@ -322,10 +322,11 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
       }
     }
   }
-  if (c1 == p.n) p.prev[b] = prev;
+  if (c1 == p.n) {  // the state for the next call, in the other buffer (chunk 0 may still be reading)
+    p.prev_out[b] = prev;
+    if (b == 0) *p.has_prev_out = 1;
+  }
 }
-
-__global__ void post_flag_kernel(int* has_prev) { *has_prev = 1; }
 
 OMEGA_STAMPS_GETTER(omega_debug_post_stamps)
 
@@ -336,7 +337,6 @@ hipError_t launch_post(const PostParams& p, hipStream_t s) {
   if (p.nb > 0)
     hipLaunchKernelGGL(post_ema_kernel, dim3((p.nb + 63) / 64, (unsigned)((p.n + kEmaChunk - 1) / kEmaChunk)), dim3(64), 0,
                        s, p);
-  hipLaunchKernelGGL(post_flag_kernel, dim3(1), dim3(1), 0, s, p.has_prev);
   return hipGetLastError();
 }
 

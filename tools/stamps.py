@@ -27,7 +27,7 @@ def main(stage):
     getter = {"kw": "omega_debug_kw_stamps", "tp": "omega_debug_spectral_stamps", "tprf": "omega_debug_rf_stamps",
               "mrfft": "omega_debug_spectral_stamps", "meters": "omega_debug_meter_stamps",
               "spectra": "omega_debug_spectra_stamps", "spectra_rf": "omega_debug_rf_stamps",
-              "post": "omega_debug_post_stamps"}[stage]
+              "post": "omega_debug_post_stamps", "drum": "omega_debug_drum_stamps"}[stage]
     if stage in ("spectra", "spectra_rf"):
         from omega_gpu import Resolution
         from omega_gpu.engine import BandTable
@@ -53,6 +53,11 @@ def main(stage):
                 pp = SpectrumPostProcessor(np.linspace(20, 20000, 512))
                 xp = torch.from_numpy(np.random.default_rng(6).random((4096, 512)).astype(np.float32)).cuda()
             pp.process(xp)
+        elif stage == "drum":
+            if "xd" not in locals():
+                xd = torch.from_numpy(np.abs(np.random.default_rng(5).standard_normal((4096, 1025))).astype(np.float32)).cuda()
+                od = torch.empty(4096, 14, dtype=torch.float64, device="cuda")
+            eng.drum_features(xd, out=od)
         elif stage == "meters":
             eng._check(lib.omega_meter_update(eng._ctx, li.data_ptr(), tpv.data_ptr(), 256, met.data_ptr(),
                                               L.MEM_DEVICE))
