@@ -256,7 +256,7 @@ hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s)
 // LDS each: the exchange buffer, reused for the contiguous magnitudes and the chroma partials; the
 // band and chroma tables are read from global memory, L1/L2-resident).
 constexpr int kSpecRfThreads = 256;
-constexpr int kSpecRfPeakWords = 12;  // peak bitmap of bins < 768: suppression reaches k / 2 < 1408 / 2
+constexpr int kSpecRfPeakWords = 12;  // peaks among bins < 64 * 12 = 768: suppression reaches k / 2 < 1536 / 2
 // OMEGA_SPEC_PREFETCH: the band-table entries and the first chroma records loaded ahead of the
 // transform (1) or where they are used (0)
 #ifndef OMEGA_SPEC_PREFETCH
@@ -283,15 +283,16 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   float2* buf = reinterpret_cast<float2*>(smem);
   float* magc = reinterpret_cast<float*>(smem);  // |X_k|, k <= K, once the untangle is done
   constexpr size_t kPartOff = ((K + 1) * sizeof(float) + 15) / 16 * 16;
-  constexpr size_t kPkwOff = kPartOff + 240 * 5 * sizeof(double);
-  constexpr size_t kClsOff = kPkwOff + kSpecRfPeakWords * sizeof(unsigned long long);
+  constexpr size_t kClsOff = kPartOff + 240 * 5 * sizeof(double);
   constexpr size_t kRedOff = kClsOff + 12 * 5 * sizeof(double);
-  static_assert(kRedOff + (NTH / 64) * sizeof(float) <= FFT::kSlots * sizeof(float2),
+  constexpr size_t kFlagOff = (kRedOff + (NTH / 64) * sizeof(float) + 15) / 16 * 16;
+  constexpr int kFlagWords = 2 * 64 * kSpecRfPeakWords / 4;  // one suppression byte per bin < c_hi
+  static_assert(kFlagOff + kFlagWords * sizeof(unsigned) <= FFT::kSlots * sizeof(float2),
                 "magnitudes, chroma partials and scratch fit the exchange buffer");
   double* part = reinterpret_cast<double*>(smem + kPartOff);  // [240][5]
-  unsigned long long* pkw = reinterpret_cast<unsigned long long*>(smem + kPkwOff);
   double(*cls)[5] = reinterpret_cast<double(*)[5]>(smem + kClsOff);
   float* redf = reinterpret_cast<float*>(smem + kRedOff);
+  unsigned* sflag = reinterpret_cast<unsigned*>(smem + kFlagOff);
   const int t = threadIdx.x;
   const int64_t fr = blockIdx.x;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + fr * p.stride);
@@ -328,17 +329,19 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   OMEGA_STAMP(1);
   FFT::template run<false, kRfTab>(v, buf, t, w1, w2b, p.rtw1, p.rtw2);
   OMEGA_STAMP(2);
-  // the first two chroma records of this thread (group-ordered), issued now for the chroma phase
-  float4 ra0 = make_float4(0.f, 0.f, 0.f, 0.f), rb0 = ra0, ra1 = ra0, rb1 = ra0;
+  // this thread's chroma records (group-ordered, j = cjf + kGrp i): the first two issued now, the
+  // next ones once the transform's registers are free (after the threshold barrier), so the
+  // accumulation waits on no load
+  constexpr int kRecPre = 2, kRecReg = 8;
+  float4 ra[kRecReg], rb[kRecReg];
   int cjf = cj0 + t % kGrp;
-  if (kSpecPrefetch && cjf < cj1) {
-    ra0 = p.crec[2 * cjf];
-    rb0 = p.crec[2 * cjf + 1];
-  }
-  if (kSpecPrefetch && cjf + kGrp < cj1) {
-    ra1 = p.crec[2 * (cjf + kGrp)];
-    rb1 = p.crec[2 * (cjf + kGrp) + 1];
-  }
+  static_for<0, kRecPre>([&](auto i) {
+    const int j = cjf + kGrp * i;
+    if (kSpecPrefetch && j < cj1) {
+      ra[i] = p.crec[2 * j];
+      rb[i] = p.crec[2 * j + 1];
+    }
+  });
   asm volatile("" ::: "memory");
   __syncthreads();
   FFT::store_spectrum(v, buf, t);
@@ -368,12 +371,32 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
       mx = fmaxf(mx, mg[q]);
     });
   }
-  mx = fmaxf(mx, mnyq);
+  mx = wave_max(fmaxf(mx, mnyq));
   __syncthreads();  // the untangle reads are done: the buffer becomes the magnitude array
   static_for<0, 16>([&](auto q) { magc[t + NTH * q] = mg[q]; });
   if (t == 0) magc[K] = mnyq;
+  if ((t & 63) == 0) redf[t >> 6] = mx;
+  for (int i = t; i < kFlagWords; i += NTH) sflag[i] = 0u;
   OMEGA_STAMP(4);
-  const float thr = block_max<NTH>(mx, redf, t) * 0.1f;  // np.max(fft) * 0.1 in float32 (barriers publish magc)
+  __syncthreads();  // publishes the magnitudes and the wave maxima
+  float thr = redf[0];
+#pragma unroll
+  for (int w = 1; w < NTH / 64; ++w) thr = fmaxf(thr, redf[w]);
+  thr *= 0.1f;  // np.max(fft) * 0.1 in float32
+  if (p.chroma_out && t < 12 * kGrp) {
+    if constexpr (!kSpecPrefetch) {
+      cj0 = p.cgoff[t / kGrp];
+      cj1 = p.cgoff[t / kGrp + 1];
+      cjf = cj0 + t % kGrp;
+    }
+    static_for<0, kRecReg>([&](auto i) {
+      const int j = cjf + kGrp * i;
+      if ((i >= kRecPre || !kSpecPrefetch) && j < cj1) {
+        ra[i] = p.crec[2 * j];
+        rb[i] = p.crec[2 * j + 1];
+      }
+    });
+  }
   OMEGA_STAMP(5);
   if (p.mag_out) {
     float* o = p.mag_out + fr * (K + 1);
@@ -434,83 +457,55 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   OMEGA_STAMP(6);
   if (!p.chroma_out) return;
   // strict local maxima above 0.1 max (chromagram.py:166-170) among bins 1..K-1 below 768 (the only
-  // ones a suppressed bin k / h, k < c_hi <= 1408, can name): bin t + NTH q is lane t % 64 of wave
-  // t / 64, its neighbours in the adjacent lanes (DPP) or, at the wave edges, in LDS; one ballot per
-  // 64 bins -> word 4 q + wave
+  // ones a suppressed bin k / h, k < c_hi <= 1536, can name): bin t + NTH q is lane t % 64 of wave
+  // t / 64, its neighbours in the adjacent lanes (DPP) or, at the wave edges, in LDS. Harmonic
+  // suppression (chromagram.py:172-187): each peak q marks bit h of bins q h inside the chromagram
+  // range (LDS atomic OR: flags commute, so one round serves every h); the accumulation applies the
+  // marks in the reference's order (h = 5, 4, 3, 2, float32 multiplies by float32(1/h)) -- the same
+  // products as its loop over peaks, on the unsuppressed magnitudes magc keeps
   {
-    const int lane = t & 63, w = t >> 6;
+    const int lane = t & 63;
     static_for<0, kSpecRfPeakWords / (NTH / 64)>([&](auto q) {
       const int k = t + NTH * q;
       const float val = mg[q];
       float lo = wave_shift1<true>(val), hi = wave_shift1<false>(val);
       if (lane == 0) lo = k >= 1 ? magc[k - 1] : 0.f;
       if (lane == 63) hi = magc[k + 1];
-      const bool pk = k >= 1 && k <= K - 1 && val > lo && val > hi && val > thr;
-      const unsigned long long m = __ballot(pk);
-      if (lane == 0) pkw[4 * q + w] = m;
+      if (k >= 1 && k <= K - 1 && val > lo && val > hi && val > thr) {
+        static_for<2, 6>([&](auto h) {
+          const int kh = k * h;
+          if (kh >= p.c_lo && kh < p.c_hi) atomicOr(&sflag[kh >> 2], 1u << (8 * (kh & 3) + h));
+        });
+      }
     });
   }
   __syncthreads();
   OMEGA_STAMP(7);
-  auto is_peak = [&](int q) { return q < 64 * kSpecRfPeakWords && (int)((pkw[q >> 6] >> (q & 63)) & 1ull); };
-  // harmonic suppression (chromagram.py:172-187) as a scatter from the peaks, in the reference's
-  // order per bin (h = 5, 4, 3, 2, float32 multiplies by float32(1/h)): round h scales bin q h of
-  // every peak q inside the chromagram range -- a bin has at most one such q per h, so a round has
-  // no conflicting writes, and the accumulation below reads the suppressed magnitudes directly
-  static_for<0, 4>([&](auto hh) {
-    constexpr int h = 5 - hh;
-    static_for<0, 64 * kSpecRfPeakWords / NTH>([&](auto qq) {
-      const int q = t + NTH * qq;
-      if (is_peak(q)) {
-        const int k = q * h;
-        if (k >= p.c_lo && k < p.c_hi) magc[k] = magc[k] * (1.0f / h);
-      }
-    });
-    __syncthreads();
-  });
+  auto suppressed = [&](int k) {
+    const unsigned f = (sflag[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+    float m = magc[k];
+    m = (f & 32u) ? m * (1.0f / 5) : m;
+    m = (f & 16u) ? m * (1.0f / 4) : m;
+    m = (f & 8u) ? m * (1.0f / 3) : m;
+    m = (f & 4u) ? m * (1.0f / 2) : m;
+    return m;
+  };
   OMEGA_STAMP(8);
   if (t < 12 * kGrp) {
     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    if constexpr (!kSpecPrefetch) {
-      cj0 = p.cgoff[t / kGrp];
-      cj1 = p.cgoff[t / kGrp + 1];
-      cjf = cj0 + t % kGrp;
-      if (cjf < cj1) {
-        ra0 = p.crec[2 * cjf];
-        rb0 = p.crec[2 * cjf + 1];
-      }
-      if (cjf + kGrp < cj1) {
-        ra1 = p.crec[2 * (cjf + kGrp)];
-        rb1 = p.crec[2 * (cjf + kGrp) + 1];
-      }
-    }
     const int j1 = cj1;
-    // group-ordered 32-byte records (weights + bin): two records per iteration, all four loads of an
-    // iteration independent (no permutation load in front of the weights)
     auto acc_rec = [&](const float4 a, const float4 b) {
-      const double ed = (double)magc[__float_as_int(b.y)];  // (suppressed above)
+      const double ed = (double)suppressed(__float_as_int(b.y));
       acc[0] = fma(ed, (double)a.x, acc[0]);
       acc[1] = fma(ed, (double)a.y, acc[1]);
       acc[2] = fma(ed, (double)a.z, acc[2]);
       acc[3] = fma(ed, (double)a.w, acc[3]);
       acc[4] = fma(ed, (double)b.x, acc[4]);
     };
-    int j = cjf;
-    if (j + kGrp < j1) {  // the prefetched pair
-      acc_rec(ra0, rb0);
-      acc_rec(ra1, rb1);
-      j += 2 * kGrp;
-    } else if (j < j1) {
-      acc_rec(ra0, rb0);
-      j += 2 * kGrp;
-    }
-    for (; j + kGrp < j1; j += 2 * kGrp) {
-      const float4 a0 = p.crec[2 * j], b0 = p.crec[2 * j + 1];
-      const float4 a1 = p.crec[2 * (j + kGrp)], b1 = p.crec[2 * (j + kGrp) + 1];
-      acc_rec(a0, b0);
-      acc_rec(a1, b1);
-    }
-    if (j < j1) acc_rec(p.crec[2 * j], p.crec[2 * j + 1]);
+    static_for<0, kRecReg>([&](auto i) {
+      if (cjf + kGrp * i < j1) acc_rec(ra[i], rb[i]);
+    });
+    for (int j = cjf + kGrp * kRecReg; j < j1; j += kGrp) acc_rec(p.crec[2 * j], p.crec[2 * j + 1]);
 #pragma unroll
     for (int o = 0; o < 5; ++o) part[t * 5 + o] = acc[o];
   }
