@@ -167,6 +167,17 @@ BiquadTab make_biquad_tab(const BiquadCoef& c, int L) {
     for (int n = 0; n < L / kKwSub; ++n) mat2_mul(A, As, As);
     for (int q = 0; q < 4; ++q) t.psub[q] = (float)As[q];
   }
+  // A^j B, j < L
+  {
+    double g[2] = {B0, B1};
+    for (int j = 0; j < L && j < 64; ++j) {
+      t.g0[j] = (float)g[0];
+      t.g1[j] = (float)g[1];
+      const double n0 = A[0] * g[0] + A[1] * g[1], n1 = A[2] * g[0] + A[3] * g[1];
+      g[0] = n0;
+      g[1] = n1;
+    }
+  }
   // An = A^L now (L <= 64)
   double P[4];
   std::memcpy(P, An, sizeof P);

@@ -91,16 +91,43 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
     e0[j] = 0.f;
     e1[j] = 0.f;
   });
-  static_for<0, LS>([&](auto i) {
+  if constexpr (kKwZtab && !kKwCorr) {
+    // e = sum_i A^(LS-1-i) B u_i over the sub-chunk's samples in processing order: two independent
+    // dot products per sub-chunk (split in halves for shorter FMA chains); the coefficients are LDS
+    // broadcast reads (pwl[64 + j].zw)
+    float f0[S], f1[S];
     static_for<0, S>([&](auto j) {
-      // sub-chunk j in processing order covers samples (REV: from the end) j*LS .. j*LS + LS - 1
-      constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
-      if constexpr (kKwCorr)
-        u[n] = bq_step(t, u[n], e0[j], e1[j]);  // zero-state outputs, corrected in step 5
-      else
-        bq_state(t, u[n], e0[j], e1[j]);
+      f0[j] = 0.f;
+      f1[j] = 0.f;
     });
-  });
+    const float2* gt = reinterpret_cast<const float2*>(pwl + 64) + 1;  // (g0, g1) of A^j B at gt[2 j]
+    static_for<0, LS>([&](auto i) {
+      // (groups of 4 broadcast reads: not all hoisted ahead into registers at once)
+      if constexpr (i % 32 == 0) asm volatile("" ::: "memory");
+      const float2 cg = gt[2 * (LS - 1 - i)];
+      const float c0 = cg.x, c1 = cg.y;
+      static_for<0, S>([&](auto j) {
+        constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
+        e0[j] = fmaf(c0, u[n], e0[j]);
+        e1[j] = fmaf(c1, u[n], e1[j]);
+      });
+    });
+    static_for<0, S>([&](auto j) {
+      e0[j] += f0[j];
+      e1[j] += f1[j];
+    });
+  } else {
+    static_for<0, LS>([&](auto i) {
+      static_for<0, S>([&](auto j) {
+        // sub-chunk j in processing order covers samples (REV: from the end) j*LS .. j*LS + LS - 1
+        constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
+        if constexpr (kKwCorr)
+          u[n] = bq_step(t, u[n], e0[j], e1[j]);  // zero-state outputs, corrected in step 5
+        else
+          bq_state(t, u[n], e0[j], e1[j]);
+      });
+    });
+  }
   float s0 = e0[0], s1 = e1[0];
   static_for<1, S>([&](auto j) {
     float r0, r1;
@@ -307,7 +334,7 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
     const BiquadTab& t = i < kPwl ? hp : shelf;
     const int l = i % kPwl;
     pwl[i / kPwl][l] = l < 64 ? make_float4(t.pw[l][0], t.pw[l][1], t.pw[l][2], t.pw[l][3])
-                              : make_float4(t.h0[l - 64], t.h1[l - 64], 0.f, 0.f);
+                              : make_float4(t.h0[l - 64], t.h1[l - 64], t.g0[l - 64], t.g1[l - 64]);
   }
   float u[L];
   if constexpr (L % 4 == 0) {

@@ -62,6 +62,7 @@ struct BiquadTab {
   float h0[64], h1[64];  // first row of A^n, n < L (zero-input response of a chunk)
   float pw[64][4];     // P^(l+1), P = A^L, row-major 2x2
   float psub[4];       // A^(L / kKwSub): the sub-chunk step inside one thread's chunk
+  float g0[64], g1[64];  // A^j B, j < L: a sample's share of its (sub-)chunk's zero-state end state
 };
 
 // each thread runs its chunk as kKwSub interleaved sub-chunks (independent recurrences: ILP)
@@ -77,8 +78,15 @@ constexpr int kKwSub = OMEGA_KW_SUB;
 #define OMEGA_KW_CORR 0
 #endif
 constexpr bool kKwCorr = OMEGA_KW_CORR != 0;
+// lfilter_pass step 1 (the zero-state end state of a chunk) as two dot products with the A^j B table
+// (LDS broadcast reads: 2 independent FMAs per sample) instead of the serial state recurrence (4
+// dependent VALU ops per sample).
+#ifndef OMEGA_KW_ZTAB
+#define OMEGA_KW_ZTAB 1
+#endif
+constexpr bool kKwZtab = OMEGA_KW_ZTAB != 0;
 // K-weighting LDS table per filter (float4 entries): [0, 64) the scan powers P^(l+1), [64, 96) the
-// first row of A^i, i < 32, as (h0, h1, -, -) -- read at the correction, not held in registers
+// first row of A^i and A^i B, i < 32, as (h0, h1, g0, g1) -- read where used, not held in registers
 constexpr int kPwl = 96;
 // register-FFT inter-pass twiddles from tables (1) or power chains (0, default). The tables cut the
 // FFT roles' VALU count (true peak 2584 -> 2396 static instructions) but ran slower on MI355X (round 2:
