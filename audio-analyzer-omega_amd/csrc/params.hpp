@@ -96,6 +96,13 @@ constexpr int kPwl = 96;
 #define OMEGA_RF_TWTAB 0
 #endif
 constexpr bool kRfTab = OMEGA_RF_TWTAB != 0;
+// true peak: lane l and lane l ^ 63 of a wave own mirror spectrum columns (t, NTH - t), so each phase's
+// mirror spectrum comes by ds_bpermute inside the wave (1) instead of an LDS exchange with two
+// workgroup barriers (0)
+#ifndef OMEGA_TP_PAIR
+#define OMEGA_TP_PAIR 1
+#endif
+constexpr bool kTpPair = OMEGA_TP_PAIR != 0;
 
 // K-weighting workgroup: up to 32 samples per thread (M/32 threads, 64..512), the chunk length L of
 // the scan tables (make_biquad_tab) follows from it.

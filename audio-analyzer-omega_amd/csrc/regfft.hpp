@@ -125,10 +125,19 @@ struct RegFFT {
   static __device__ __forceinline__ void run(float2 (&v)[16], float2* buf, int t, float2 w1, float2 w2,
                                              const float4* __restrict__ tw1 = nullptr,
                                              const float4* __restrict__ tw2 = nullptr) {
+    run2<SYNC, TAB>(v, buf, t, t, w1, w2, tw1, tw2);
+  }
+  // run() with the pass-1 input column t1 (v[r] = x[t1 + NTH r], w1 = W_K^t1) decoupled from the
+  // thread's pass-2/3 role t (w2 = W_K^{16 (t mod L)}): any bijection tid -> t1 (the true peak pairs
+  // mirror columns t1, NTH - t1 inside one wave).
+  template <bool SYNC = false, bool TAB = false>
+  static __device__ __forceinline__ void run2(float2 (&v)[16], float2* buf, int t1, int t, float2 w1, float2 w2,
+                                              const float4* __restrict__ tw1 = nullptr,
+                                              const float4* __restrict__ tw2 = nullptr) {
     // pass 1
     if constexpr (TAB) {
       float4 q[8];
-      load_tab(q, tw1 + t, NTH);
+      load_tab(q, tw1 + t1, NTH);
       dft16(v);
       twiddle_tab(v, q);
     } else {
@@ -137,11 +146,11 @@ struct RegFFT {
     }
     if constexpr (SYNC) __syncthreads();
     if constexpr (TIGHT) {
-      float2* b0 = buf + t;
-      float2* b1 = buf + (t ^ 16);
+      float2* b0 = buf + t1;
+      float2* b1 = buf + (t1 ^ 16);
       static_for<0, 16>([&](auto k1) { (k1 & 1 ? b1 : b0)[256 * k1] = v[k1]; });
     } else {
-      float2* b = buf + t;
+      float2* b = buf + t1;
       static_for<0, 16>([&](auto k1) { b[P1 * k1] = v[k1]; });
     }
     __syncthreads();

@@ -33,10 +33,22 @@ namespace omega {
 template <int K>
 constexpr size_t lds_bytes() { return (RegFFT<K>::kSlots + 8) * sizeof(float2) + 64; }
 
+// kTpPair column map: thread tid = 64 w + l owns spectrum column t = 32 w + l (l < 32), and lane
+// l ^ 63 the mirror column NTH - t (column NTH / 2 for t = 0); columns 0 and NTH / 2 mirror themselves
+template <int NTH>
+__device__ __forceinline__ int tp_column(int tid) {
+  if constexpr (!kTpPair) return tid;
+  const int w = tid >> 6, l = tid & 63;
+  if (l < 32) return 32 * w + l;
+  const int a = 32 * w + (63 - l);
+  return a == 0 ? NTH / 2 : NTH - a;
+}
+
 template <int K>
-__device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_t cf, int t, char* smem) {
+__device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_t cf, int tid, char* smem) {
   using FFT = RegFFT<K>;
   constexpr int NTH = FFT::NTH, M = 2 * K;
+  const int t = tp_column<NTH>(tid);  // this thread's spectrum column (pass-1 input, untangle, phases)
   float2* buf = reinterpret_cast<float2*>(smem);
   float* red = reinterpret_cast<float*>(smem + (FFT::kSlots + 8) * sizeof(float2));
   const int64_t f = cf / p.C, c = cf % p.C;
@@ -48,7 +60,7 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
   OMEGA_STAMP(0);
   // the thread's twiddle bases first: their (L2-resident) loads return while the frame streams in,
   // instead of behind it (vmcnt waits in issue order) at the first pass's twiddle multiply
-  const float2 w1 = twK[t], w2 = twK[16 * (t % FFT::L)];
+  const float2 w1 = twK[t], w2 = twK[16 * (tid % FFT::L)];
   const float2 wm = twM[t];     // W_M^t
   const float2 rho = p.rot[t];  // e^{2 pi i t / 4M}
   asm volatile("" ::: "memory");  // (keeps the scheduler from sinking them behind the frame loads)
@@ -59,11 +71,11 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
   OMEGA_STAMP(1);
   const float4* __restrict__ rt1 = p.rtw1[K == 8192];
   const float4* __restrict__ rt2 = p.rtw2[K == 8192];
-  FFT::template run<false, kRfTab>(v, buf, t, w1, w2, rt1, rt2);
+  FFT::template run2<false, kRfTab>(v, buf, t, tid, w1, w2, rt1, rt2);
   OMEGA_STAMP(2);
   // natural-order spectrum -> X_k on k in S_t
   __syncthreads();
-  FFT::store_spectrum(v, buf, t);
+  FFT::store_spectrum(v, buf, tid);
   __syncthreads();
   OMEGA_STAMP(3);
   float xn = 0.f;  // X_K (thread 0)
@@ -92,14 +104,17 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
   // i e^{2 pi i t / M} / 2: alpha_k = (1/2, 0) + (that) e^{2 pi i r / 32}
   const float2 hz = make_float2(0.5f * wm.y, 0.5f * wm.x);
   float fmx = 0.f;
+  // kTpPair: byte address of the lane holding the mirror column (itself for columns 0 and NTH / 2)
+  const int lane = tid & 63;
+  const int mir_addr = 4 * ((t == 0 || t == NTH / 2) ? lane : lane ^ 63);
   OMEGA_STAMP(4);
 #pragma unroll 1
   for (int P = 1; P <= 3; ++P) {
     // opaque per-iteration copies: keep the inlined FFT's address arithmetic and twiddle powers
     // inside the loop instead of hoisted and pinned in VGPRs across it
-    int tl = t;
+    int tl = t, tidl = tid;
     float2 w1l = w1, w2l = w2, rhol = rho, hzl = hz;
-    asm volatile("" : "+v"(tl), "+v"(w1l.x), "+v"(w1l.y), "+v"(w2l.x), "+v"(w2l.y));
+    asm volatile("" : "+v"(tl), "+v"(tidl), "+v"(w1l.x), "+v"(w1l.y), "+v"(w2l.x), "+v"(w2l.y));
     asm volatile("" : "+v"(rhol.x), "+v"(rhol.y), "+v"(hzl.x), "+v"(hzl.y));
     static_for<0, 16>([&](auto r) {
       const float2 rk = cmul(rhol, make_float2(kCos128[r], kSin128[r]));
@@ -107,22 +122,36 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
     });
     if (!((p.tp_phases >> P) & 1)) continue;  // phase not requested (oversampling 2 or 1)
     OMEGA_STAMP(1 + 4 * P);
-    __syncthreads();  // the previous transform's last exchange reads are done
-    {
-      float2* bo = buf + FFT::s3(tl);
-      static_for<0, 16>([&](auto r) { bo[FFT::o3(r)] = y[r]; });
-    }
-    __syncthreads();
-    OMEGA_STAMP(2 + 4 * P);
     const float cp = P == 1 ? 7.071067812e-01f : (P == 2 ? 0.f : -7.071067812e-01f);
     const float2* bm = buf + FFT::s3m(tl);
+    if constexpr (!kTpPair) {
+      __syncthreads();  // the previous transform's last exchange reads are done
+      float2* bo = buf + FFT::s3(tl);
+      static_for<0, 16>([&](auto r) { bo[FFT::o3(r)] = y[r]; });
+      __syncthreads();
+    }
+    OMEGA_STAMP(2 + 4 * P);
     static_for<0, 16>([&](auto r) {
-      float2 yp = cconj(bm[FFT::o3(15 - r)]);
-      if constexpr (r == 0) {
-        if (tl == 0) yp = make_float2(xn * cp, 0.f);
-      }
-      if constexpr (K == 8192 && r == 8) {
-        if (tl == 0) yp = cconj(y[8]);
+      float2 yp;
+      if constexpr (kTpPair) {
+        // Y_{K-k}, k = t + NTH r: register 15 - r of the mirror lane (t >= 1); column 0 holds its own
+        // mirrors in register 16 - r (r >= 1)
+        const float2 m = y[15 - r];
+        yp = make_float2(__int_as_float(__builtin_amdgcn_ds_bpermute(mir_addr, __float_as_int(m.x))),
+                         -__int_as_float(__builtin_amdgcn_ds_bpermute(mir_addr, __float_as_int(m.y))));
+        if constexpr (r == 0) {
+          if (tl == 0) yp = make_float2(xn * cp, 0.f);
+        } else {
+          if (tl == 0) yp = cconj(y[16 - r]);
+        }
+      } else {
+        yp = cconj(bm[FFT::o3(15 - r)]);
+        if constexpr (r == 0) {
+          if (tl == 0) yp = make_float2(xn * cp, 0.f);
+        }
+        if constexpr (K == 8192 && r == 8) {
+          if (tl == 0) yp = cconj(y[8]);
+        }
       }
       const float2 g = twc<-r, 32>(hzl);  // (i e_t / 2) e^{2 pi i r / 32}
       const float2 al = make_float2(0.5f + g.x, g.y);
@@ -130,12 +159,12 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
       v[r] = cconj(cadd(yp, cmul(al, d)));
     });
     OMEGA_STAMP(3 + 4 * P);
-    FFT::template run<true, kRfTab>(v, buf, tl, w1l, w2l, rt1, rt2);
+    FFT::template run2<true, kRfTab>(v, buf, tl, tidl, w1l, w2l, rt1, rt2);
     static_for<0, 16>([&](auto m) { fmx = fmaxf(fmx, fmaxf(fabsf(v[m].x), fabsf(v[m].y))); });
     OMEGA_STAMP(4 + 4 * P);
   }
-  const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, t);
-  if (t == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
+  const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
+  if (tid == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
 }
 
 template <int K>
