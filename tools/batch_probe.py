@@ -14,7 +14,8 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 STAGES = {"kw": dict(combined=False, true_peak=False), "tp": dict(combined=False, lufs=False),
-          "res": dict(lufs=False, true_peak=False), "all": dict()}
+          "res": dict(lufs=False, true_peak=False), "kw+tp": dict(combined=False),
+          "kw+res": dict(true_peak=False), "tp+res": dict(lufs=False), "all": dict()}
 
 
 def timed(fn, reps):
