@@ -7,13 +7,14 @@
 //   rfft: z[n] = x[2n] + i x[2n+1], Z = FFT_K(z) (input straight from HBM into registers), Z written
 //     in natural order, then X_k = E + W_M^k O from (Z_k, Z_{K-k}) for k in S_t (X_0 and the Nyquist
 //     bin X_K on thread 0).
-//   phase p = 1..3: Y_k = X_k rho_k^p (running product, rho_k = e^{2 pi i k / 4M}); Y written to LDS,
-//     the mirror Y_{K-k} read back; the packed inverse spectrum
+//   phase p = 1..3: Y_k = X_k rho_k^p (running product, rho_k = e^{2 pi i k / 4M}); the mirror Y_{K-k}
+//     from the lane that owns column NTH - t (tp_column: lanes l and l ^ 63 of a wave hold mirror
+//     columns, ds_bpermute, no LDS exchange); the packed inverse spectrum
 //       Z'_k = conj(Y' + alpha_k (Y_k - Y')),  Y' = conj(Y_{K-k}) (Nyquist share X_K cos(pi p/4) at
 //       k = 0), alpha_k = (1 + i e^{2 pi i k / M}) / 2
 //     is the first pass's input, in registers; the forward FFT of Z' is conj(K * y_p) packed, reduced
 //     to max |.| from the last pass's registers.
-// Per frame: 4 transforms, 12 LDS exchanges of 64 KiB (the old 1024-thread radix-8 kernel: 19).
+// Per frame: 4 transforms, 9 LDS exchanges of 64 KiB (the old 1024-thread radix-8 kernel: 19).
 #include <cstdlib>
 
 #include "stamps.hpp"
