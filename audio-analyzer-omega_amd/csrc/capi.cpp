@@ -222,6 +222,15 @@ struct omega_ctx {
   unsigned* d_kw_done = nullptr;  // batch_kernel's K-weighting workgroups count themselves in here
   unsigned kw_issued = 0;         // K-weighting workgroups launched with the count on (wraps)
   unsigned q_issued = 0;          // LUFS-meter query workgroups launched with the count on (d_kw_done[1])
+  unsigned p_issued = 0;          // tail layout: meter-prep workgroups launched with the count on (d_kw_done[2])
+  unsigned tp_issued = 0;         // batch true-peak workgroups launched with the count on (d_kw_done[3])
+  unsigned wg_issued = 0;         // batch workgroups launched with the join count on (d_kw_done[4])
+  // the true-peak meter query on the side stream and a join in the batch kernel's last workgroup instead
+  // of the query after the batch (OMEGA_BATCH_JOIN=1): measured slower (85.2-87.3 vs 79.9-81.2 us per
+  // step) -- the query workgroups wait for the true-peak count while resident, each holding the
+  // registers of half a batch workgroup slot
+  bool batch_join = false;
+  bool meter_tail = false;        // tail layout: prep alone beside the batch, both query parts after it
   // device-side poll expiry flags (host-mapped: [0] meter prep, [1] join), checked by
   // check_device_err; the poll bound (OMEGA_POLL_LIMIT, a test knob)
   unsigned* h_err = nullptr;
@@ -711,7 +720,7 @@ int build_meter_state(omega_ctx* c) {
   if (!e) e = dalloc(c, &c->d_next, C);
   if (!e) e = dalloc(c, &c->d_gcount, (size_t)C * (kMeterSeqCap + 1));
   if (!e) e = dalloc(c, &c->d_gsum, (size_t)C * (kMeterSeqCap + 1));
-  if (!e) e = dalloc(c, &c->d_kw_done, 4);
+  if (!e) e = dalloc(c, &c->d_kw_done, 8);
   if (e) return e;
   if (!c->h_err) {
     HIPC(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_err), 2 * sizeof(unsigned),
@@ -719,8 +728,8 @@ int build_meter_state(omega_ctx* c) {
     c->h_err[0] = c->h_err[1] = 0;
     HIPC(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_err), c->h_err, 0));
   }
-  HIPC(c, hipMemset(c->d_kw_done, 0, 4 * sizeof(unsigned)));
-  c->kw_issued = c->q_issued = 0;
+  HIPC(c, hipMemset(c->d_kw_done, 0, 8 * sizeof(unsigned)));
+  c->kw_issued = c->q_issued = c->p_issued = c->tp_issued = c->wg_issued = 0;
   return omega_meter_reset(c);
 }
 
@@ -890,7 +899,7 @@ bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams&
 // layout with events 99.2. Mixing the
 // latency-bound K-weighting scans with transform work is what pays (K-weighting alone 25.7 us, the
 // true peak 37, the resolutions 26.5; one batch launch of all three 73.9).
-int enqueue_batch(omega_ctx* c, const SpectralParams& sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
+int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
                   const float* tp, double* meters, hipStream_t s, int mr, bool do_tp, bool do_kw) {
   const int64_t n = sp.n_cf;
   const int order = c->batch_order;
@@ -933,11 +942,24 @@ int enqueue_batch(omega_ctx* c, const SpectralParams& sp, KWeightParams kp, int 
   const int64_t grid = end + nwg;
   if (grid > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
   std::vector<MeterPrepParams> mc;
+  bool tail = false;
   if (meters) {
     mc = meter_chunks(c, lufs, tp, n_frames, meters);
     kp.kw_done = c->d_kw_done;
     c->kw_issued += (unsigned)n;
-    for (size_t i = 0; i < mc.size(); ++i) {
+    // tail layout (one meter chunk: a second chunk's prep would overwrite the per-batch scratch before
+    // the first chunk's query ran): the prep waits for the K-weighting count beside the batch and counts
+    // itself in; both query parts run after the batch on `s`
+    tail = c->meter_tail && mc.size() == 1;
+    if (tail) {
+      MeterPrepParams p = mc[0];
+      p.wait_ctr = c->d_kw_done;
+      p.wait_target = c->kw_issued;
+      p.q_done = c->d_kw_done + 2;
+      HIPC(c, launch_meter_prep(p, c->fork[0]));
+      c->p_issued += (unsigned)p.C;
+    }
+    for (size_t i = 0; i < mc.size() && !tail; ++i) {
       MeterPrepParams p = mc[i];
       if (i == 0) {
         p.wait_ctr = c->d_kw_done;
@@ -950,6 +972,32 @@ int enqueue_batch(omega_ctx* c, const SpectralParams& sp, KWeightParams kp, int 
       c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);  // (counted once it is enqueued)
     }
   }
+  // the join (default): the true-peak meter queries follow on the side stream (the first waits for the
+  // batch's true-peak count) and the batch kernel's last workgroup waits for every query workgroup, so
+  // `s` ends with the batch kernel (no kernel after it on the critical path)
+  const bool join = meters && !tail && c->batch_join && do_tp && grid > 0;
+  if (join) {
+    sp.tp_done = c->d_kw_done + 3;
+    c->tp_issued += (unsigned)n;
+    for (size_t i = 0; i < mc.size(); ++i) {
+      MeterPrepParams p = mc[i];
+      p.parts = 2;
+      p.q_done = c->d_kw_done + 1;
+      if (i == 0) {
+        p.start_ctr = c->d_kw_done + 3;
+        p.start_target = c->tp_issued;
+      }
+      HIPC(c, launch_meter_query(p, c->fork[0]));
+      c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);
+    }
+    c->wg_issued += (unsigned)grid;
+    bp.wg_done = c->d_kw_done + 4;
+    bp.wg_target = c->wg_issued;
+    bp.join_ctr = c->d_kw_done + 1;
+    bp.join_target = c->q_issued;
+    bp.poll_limit = c->poll_limit;
+    bp.err_word = c->d_err;
+  }
   {
     hipError_t le = hipSuccess;
     if (do_kw && !kw_in_batch) le = launch_kweight(W, kp, s);
@@ -958,8 +1006,21 @@ int enqueue_batch(omega_ctx* c, const SpectralParams& sp, KWeightParams kp, int 
       // the prep kernel already waits for this batch's count: publish it, so that it (and every later
       // call's target) stays in step with the device counter instead of timing out
       if (meters) (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
+      if (join) {  // the same for the side stream's true-peak query and the join count
+        (void)hipMemcpy(c->d_kw_done + 3, &c->tp_issued, sizeof(unsigned), hipMemcpyHostToDevice);
+        (void)hipMemcpy(c->d_kw_done + 4, &c->wg_issued, sizeof(unsigned), hipMemcpyHostToDevice);
+      }
       return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
     }
+  }
+  if (join) return 0;
+  if (tail) {
+    MeterPrepParams p = mc[0];
+    p.parts = 3;
+    p.start_ctr = c->d_kw_done + 2;
+    p.start_target = c->p_issued;
+    HIPC(c, launch_meter_query(p, s));
+    return 0;
   }
   for (size_t i = 0; i < mc.size(); ++i) {
     MeterPrepParams p = mc[i];
@@ -1113,6 +1174,8 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   if (const char* rs = std::getenv("OMEGA_RF_SIZES")) c->rf_sizes = std::atoi(rs) & ((1 << 14) | (1 << 13));
   if (const char* gr = std::getenv("OMEGA_GRAPHS")) c->use_graph = std::atoi(gr) != 0;
   if (const char* bo = std::getenv("OMEGA_BATCH_ORDER")) c->batch_order = std::atoi(bo);
+  if (const char* mt = std::getenv("OMEGA_METER_TAIL")) c->meter_tail = std::atoi(mt) != 0;
+  if (const char* bj = std::getenv("OMEGA_BATCH_JOIN")) c->batch_join = std::atoi(bj) != 0;
   if (const char* pl = std::getenv("OMEGA_POLL_LIMIT")) c->poll_limit = std::atoi(pl) > 0 ? std::atoi(pl) : 1;
   if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
     const int v = std::atoi(lay);

@@ -407,6 +407,17 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   for (int i = tid; i < klen; i += 1024) p.hist_l_out[(int64_t)c * p.HL + i] = V[L - klen + i];
   if (tid == 0) p.n_l_out[c] = klen;
   OMEGA_STAMP(7);
+  if (p.q_done) {
+    // (tail layout) count this channel's prep in for the query kernel on the other stream: every
+    // wave's stores drained, then one agent-scope release before the add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(p.q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 __device__ __forceinline__ double lerp_pct(double a, double b, double gamma) {
@@ -526,6 +537,23 @@ __device__ __forceinline__ void meter_query_body(const MeterPrepParams& p) {
 }
 
 __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
+  if (p.start_ctr) {
+    // (tail layout) the prep kernel runs on another stream: wait (bounded) until it has counted in
+    if (threadIdx.x == 0) {
+      bool met = false;
+      for (int i = 0; i < p.poll_limit; ++i) {
+        if ((int)(__hip_atomic_load(p.start_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - p.start_target) >= 0) {
+          met = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      if (!met && p.err_word)
+        __hip_atomic_store(p.err_word + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+  }
   meter_query_body(p);
   if (p.q_done) {
     // count this workgroup's outputs in for the device-side join: every wave's stores drained, then one

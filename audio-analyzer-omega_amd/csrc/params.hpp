@@ -52,6 +52,9 @@ struct SpectralParams {
   const float4* rtw1[2];
   const float4* rtw2[2];
   int rf_sizes;  // host-side launch choice: bit log2(N) set = resolution size N runs on the register-FFT kernel
+  // batch_kernel's true-peak role: when set, the value is stored write-through and the workgroup adds 1
+  // after it (the true-peak meter query on the side stream waits for the batch's count)
+  unsigned* tp_done;
 };
 
 // One zero-phase biquad (filtfilt with scipy's defaults) in state-space form:
@@ -183,6 +186,10 @@ struct MeterPrepParams {
   unsigned* q_done;
   unsigned* join_ctr;
   unsigned join_target;
+  // tail layout (omega_ctx::meter_tail): meter_prep_kernel counts itself into q_done when set;
+  // meter_query_kernel waits (every workgroup, bounded) until (int)(*start_ctr - start_target) >= 0
+  unsigned* start_ctr;
+  unsigned start_target;
   // bounded polls: at most poll_limit iterations; on expiry the kernel stores 1 into err_word[0] (prep)
   // or err_word[1] (join) -- host-mapped memory the host checks in omega_synchronize and the next call
   // (OMEGA_EHIP instead of silently stale meters)
@@ -249,6 +256,15 @@ struct BatchPlan {
   int roles[2][3];
   int mr_res;
   MultiPlan multi;
+  // the join (omega_ctx::batch_join): every workgroup counts itself into wg_done when it is finished;
+  // the one that completes the count (wg_target) does not finish before (int)(*join_ctr - join_target)
+  // >= 0 (the side stream's meter queries), bounded by poll_limit, expiry -> err_word[1]
+  unsigned* wg_done;
+  unsigned wg_target;
+  unsigned* join_ctr;
+  unsigned join_target;
+  int poll_limit;
+  unsigned* err_word;
 };
 
 // Fused spectrum analysis (cfg3): windowed rfft magnitude (A13) -> log-band max (A10) and raw

@@ -165,7 +165,17 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
     OMEGA_STAMP(4 + 4 * P);
   }
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
-  if (tid == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
+  if (tid == 0) {
+    const float db = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
+    if (p.tp_done) {  // write-through, drained, then counted in (see SpectralParams::tp_done)
+      __hip_atomic_store(reinterpret_cast<unsigned*>(p.tp_out + cf), __float_as_uint(db), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(p.tp_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      p.tp_out[cf] = db;
+    }
+  }
 }
 
 template <int K>
@@ -633,8 +643,7 @@ void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
   kw_count_in(kp, tid);
 }
 
-__global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams sp, KWeightParams kp, BatchPlan bp) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, char* smem) {
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
   if (b < bp.seg_begin[2]) {
@@ -666,6 +675,32 @@ __global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams 
     case 4096: batch_multi<2048>(sp, r, wg, tid, buf); break;
     case 8192: batch_multi<4096>(sp, r, wg, tid, buf); break;
     default: break;
+  }
+}
+
+__global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams sp, KWeightParams kp, BatchPlan bp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  batch_body(sp, kp, bp, smem);
+  if (bp.wg_done) {
+    // the join: the workgroup that finishes the launch's count waits for the side stream's meter
+    // queries, so this stream completes after them (no stream event, no kernel after the batch)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(bp.wg_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old + 1u == bp.wg_target) {
+        bool met = false;
+        for (int i = 0; i < bp.poll_limit; ++i) {
+          if ((int)(__hip_atomic_load(bp.join_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - bp.join_target) >= 0) {
+            met = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(4);
+        }
+        if (!met && bp.err_word)
+          __hip_atomic_store(bp.err_word + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+    }
   }
 }
 
