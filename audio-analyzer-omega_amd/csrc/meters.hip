@@ -500,26 +500,37 @@ __device__ __forceinline__ void meter_query_body(const MeterPrepParams& p) {
     int below[4] = {0, 0, 0, 0};  // member extras of merged rank < want
     bool found[4] = {false, false, false, false};
     int jb = 0;
-    for (int i0 = 0; i0 < ne; i0 += 64) {
-      const int i = i0 + lane;
-      MeterExt e{0.f, 0u, 0, 0};
-      bool mem = false;
-      if (i < ne) {
-        e = ext[i];
-        mem = (uint32_t)(e.t - lo) <= hi - lo && !(has_core && (uint32_t)(e.t - clo) <= chi - clo);
-      }
-      const unsigned long long bm = __ballot(mem);
-      const int rank = jb + __popcll(bm & ((1ull << lane) - 1ull)) + e.rc;
+    // kExtRounds rounds of 64 extras loaded together (one L2 latency per group instead of per round:
+    // the query runs beside the batch kernel, and its resident time costs the batch register slots)
+#ifndef OMEGA_EXT_ROUNDS
+#define OMEGA_EXT_ROUNDS 4
+#endif
+    constexpr int kExtRounds = OMEGA_EXT_ROUNDS;
+    for (int g0 = 0; g0 < ne; g0 += 64 * kExtRounds) {
+      MeterExt eg[kExtRounds];
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        below[w] += __popcll(__ballot(mem && rank < want[w]));
-        const unsigned long long hit = __ballot(mem && rank == want[w]);
-        if (hit) {
-          found[w] = true;
-          val[w] = __shfl(e.v, __ffsll((long long)hit) - 1, 64);
-        }
+      for (int q = 0; q < kExtRounds; ++q) {
+        const int i = g0 + 64 * q + lane;
+        eg[q] = i < ne ? ext[i] : MeterExt{0.f, 0u, 0, 0};
       }
-      jb += __popcll(bm);
+#pragma unroll
+      for (int q = 0; q < kExtRounds; ++q) {
+        const MeterExt e = eg[q];
+        const bool mem = g0 + 64 * q + lane < ne && (uint32_t)(e.t - lo) <= hi - lo &&
+                         !(has_core && (uint32_t)(e.t - clo) <= chi - clo);
+        const unsigned long long bm = __ballot(mem);
+        const int rank = jb + __popcll(bm & ((1ull << lane) - 1ull)) + e.rc;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          below[w] += __popcll(__ballot(mem && rank < want[w]));
+          const unsigned long long hit = __ballot(mem && rank == want[w]);
+          if (hit) {
+            found[w] = true;
+            val[w] = __shfl(e.v, __ffsll((long long)hit) - 1, 64);
+          }
+        }
+        jb += __popcll(bm);
+      }
     }
     const float* core = p.core + (int64_t)c * kSeqCap;
 #pragma unroll
