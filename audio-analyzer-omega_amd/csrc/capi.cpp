@@ -230,6 +230,10 @@ struct omega_ctx {
   // step) -- the query workgroups wait for the true-peak count while resident, each holding the
   // registers of half a batch workgroup slot
   bool batch_join = false;
+  // the true-peak meter as the batch grid's last workgroup instead of a kernel after the batch
+  // (OMEGA_TP_METER_BATCH=1; one meter chunk): parity green, measured slower (86-88 vs 80-83 us per
+  // step, the window maxima per thread or staged in LDS alike)
+  bool tp_meter_in_batch = false;
   bool meter_tail = false;        // tail layout: prep alone beside the batch, both query parts after it
   // device-side poll expiry flags (host-mapped: [0] meter prep, [1] join), checked by
   // check_device_err; the poll bound (OMEGA_POLL_LIMIT, a test knob)
@@ -976,6 +980,23 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   // batch's true-peak count) and the batch kernel's last workgroup waits for every query workgroup, so
   // `s` ends with the batch kernel (no kernel after it on the critical path)
   const bool join = meters && !tail && c->batch_join && do_tp && grid > 0;
+  // (the role stages history ++ batch of one channel in the batch kernel's LDS)
+  const bool tpm = meters && !tail && !join && c->tp_meter_in_batch && do_tp && grid > 0 && mc.size() == 1 &&
+                   (size_t)(mc[0].HT + mc[0].n_frames) * sizeof(float) <= 65536;
+  int64_t grid_all = grid;
+  bp.tpm_wg = -1;
+  if (tpm) {
+    sp.tp_done = c->d_kw_done + 3;
+    c->tp_issued += (unsigned)n;
+    bp.tpm_wg = (int)grid;
+    bp.tp_target = c->tp_issued;
+    bp.mq = mc[0];
+    bp.join_ctr = c->d_kw_done + 1;
+    bp.join_target = c->q_issued;
+    bp.poll_limit = c->poll_limit;
+    bp.err_word = c->d_err;
+    grid_all = grid + 1;
+  }
   if (join) {
     sp.tp_done = c->d_kw_done + 3;
     c->tp_issued += (unsigned)n;
@@ -1001,19 +1022,19 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   {
     hipError_t le = hipSuccess;
     if (do_kw && !kw_in_batch) le = launch_kweight(W, kp, s);
-    if (le == hipSuccess && grid > 0) le = launch_batch(sp, kp, bp, (int)grid, s);
+    if (le == hipSuccess && grid > 0) le = launch_batch(sp, kp, bp, (int)grid_all, s);
     if (le != hipSuccess) {
       // the prep kernel already waits for this batch's count: publish it, so that it (and every later
       // call's target) stays in step with the device counter instead of timing out
       if (meters) (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
-      if (join) {  // the same for the side stream's true-peak query and the join count
+      if (join || tpm) {  // the same for the side stream's true-peak query and the join count
         (void)hipMemcpy(c->d_kw_done + 3, &c->tp_issued, sizeof(unsigned), hipMemcpyHostToDevice);
         (void)hipMemcpy(c->d_kw_done + 4, &c->wg_issued, sizeof(unsigned), hipMemcpyHostToDevice);
       }
       return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
     }
   }
-  if (join) return 0;
+  if (join || tpm) return 0;
   if (tail) {
     MeterPrepParams p = mc[0];
     p.parts = 3;
@@ -1176,6 +1197,7 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   if (const char* bo = std::getenv("OMEGA_BATCH_ORDER")) c->batch_order = std::atoi(bo);
   if (const char* mt = std::getenv("OMEGA_METER_TAIL")) c->meter_tail = std::atoi(mt) != 0;
   if (const char* bj = std::getenv("OMEGA_BATCH_JOIN")) c->batch_join = std::atoi(bj) != 0;
+  if (const char* tb = std::getenv("OMEGA_TP_METER_BATCH")) c->tp_meter_in_batch = std::atoi(tb) != 0;
   if (const char* pl = std::getenv("OMEGA_POLL_LIMIT")) c->poll_limit = std::atoi(pl) > 0 ? std::atoi(pl) : 1;
   if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
     const int v = std::atoi(lay);

@@ -265,6 +265,14 @@ struct BatchPlan {
   unsigned join_target;
   int poll_limit;
   unsigned* err_word;
+  // the true-peak meter as the grid's last workgroup (omega_ctx::tp_meter_in_batch, one meter chunk):
+  // workgroup tpm_wg (-1: none) waits (bounded) for the batch's true-peak count (SpectralParams::
+  // tp_done >= tp_target) and for the side stream's LUFS-query count (join_ctr >= join_target), then
+  // computes column 4 of the meters and rolls the true-peak history of mq, as meter_query_kernel's
+  // true-peak part would after the batch
+  int tpm_wg;
+  unsigned tp_target;
+  MeterPrepParams mq;
 };
 
 // Fused spectrum analysis (cfg3): windowed rfft magnitude (A13) -> log-band max (A10) and raw

@@ -643,9 +643,60 @@ void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
   kw_count_in(kp, tid);
 }
 
+// bounded poll of one lane: (int)(*ctr - target) >= 0, expiry -> err_word[1]
+__device__ __forceinline__ void batch_wait(const unsigned* ctr, unsigned target, int limit, unsigned* err) {
+  bool met = false;
+  for (int i = 0; i < limit; ++i) {
+    if ((int)(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) {
+      met = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  if (!met && err) __hip_atomic_store(err + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The true-peak meter (professional_meters.py:265-279: max over the last peak_len true peaks of the
+// stream, history ++ batch) for every (frame, channel) of the batch and the stream's true-peak history
+// rolled -- meter_query_kernel's true-peak part as the batch's last role. Per channel the sequence
+// history ++ batch is staged in LDS (one coalesced pass), then one thread per frame takes its window max.
+__device__ __forceinline__ void batch_tp_meter(const SpectralParams& sp, const BatchPlan& bp, int tid, char* smem) {
+  const MeterPrepParams& p = bp.mq;
+  if (tid == 0) {
+    batch_wait(sp.tp_done, bp.tp_target, bp.poll_limit, bp.err_word);
+    batch_wait(bp.join_ctr, bp.join_target, bp.poll_limit, bp.err_word);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  float* seq = reinterpret_cast<float*>(smem);  // nt + F <= HT + kMeterChunk floats
+  const int C = p.C;
+  const int F = (int)p.n_frames;
+  for (int c = 0; c < C; ++c) {
+    const int nt = p.n_t_in[c];
+    const int tt = nt + F;
+    for (int i = tid; i < tt; i += kBatchThreads)
+      seq[i] = i < nt ? p.hist_t_in[(int64_t)c * p.HT + i] : p.tp[(int64_t)(i - nt) * C + c];
+    __syncthreads();
+    const int ktl = min(p.HT, tt);
+    for (int i = tid; i < ktl; i += kBatchThreads) p.hist_t_out[(int64_t)c * p.HT + i] = seq[tt - ktl + i];
+    if (tid == 0) p.n_t_out[c] = ktl;
+    for (int f = tid; f < F; f += kBatchThreads) {
+      const int ntp = nt + f + 1, wt = min(p.peak_len, ntp);
+      float tpm = -INFINITY;
+      for (int i = ntp - wt; i < ntp; ++i) tpm = fmaxf(tpm, seq[i]);
+      p.out[((int64_t)f * C + c) * 5 + 4] = (double)tpm;
+    }
+    __syncthreads();  // (seq is restaged for the next channel)
+  }
+}
+
 __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, char* smem) {
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
+  if (b == bp.tpm_wg) {
+    batch_tp_meter(sp, bp, tid, smem);
+    return;
+  }
   if (b < bp.seg_begin[2]) {
     const int sg = b < bp.seg_begin[1] ? 0 : 1;
     const int j = b - bp.seg_begin[sg], nr = bp.n_roles[sg];

@@ -1,11 +1,10 @@
 set -e
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -x -k "meter or cfg2 or cfg4 or stream or golden or lufs" > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -x > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
 tail -2 gpurun_out/ab_tests.log
 B="--steps 300 --warmup 30 --no-cpu-baseline --no-cfg3 --no-cfg4 --no-cfg5"
-for rep in 1 2 3; do for v in "" ext1; do
-  OMEGA_VARIANT=$v timeout -k 5 120 python bench.py $B > gpurun_out/ab_b.json
-  python -c "import json,sys; d=json.load(open('gpurun_out/ab_b.json')); print('variant', sys.argv[1], round(d['value']), 'cf/s', round(d['ms_per_step']*1e3,1), 'us/step')" "[$v]"
+for rep in 1 2 3; do for t in 0 1; do
+  OMEGA_TP_METER_BATCH=$t timeout -k 5 120 python bench.py $B > gpurun_out/ab_b.json
+  python -c "import json,sys; d=json.load(open('gpurun_out/ab_b.json')); print('tpm', sys.argv[1], round(d['value']), 'cf/s', round(d['ms_per_step']*1e3,1), 'us/step')" $t
 done; done
-timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/abtrace -o run -- python bench.py $B --steps 50 --warmup 5 > gpurun_out/abtrace.log 2>&1
