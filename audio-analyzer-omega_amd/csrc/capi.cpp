@@ -979,13 +979,16 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   // the join (default): the true-peak meter queries follow on the side stream (the first waits for the
   // batch's true-peak count) and the batch kernel's last workgroup waits for every query workgroup, so
   // `s` ends with the batch kernel (no kernel after it on the critical path)
-  const bool join = meters && !tail && c->batch_join && do_tp && grid > 0;
+  const bool join = kBatchExtras && meters && !tail && c->batch_join && do_tp && grid > 0;
   // (the role stages history ++ batch of one channel in the batch kernel's LDS)
-  const bool tpm = meters && !tail && !join && c->tp_meter_in_batch && do_tp && grid > 0 && mc.size() == 1 &&
+  const bool tpm = kBatchExtras && meters && !tail && !join && c->tp_meter_in_batch && do_tp && grid > 0 && mc.size() == 1 &&
                    (size_t)(mc[0].HT + mc[0].n_frames) * sizeof(float) <= 65536;
   int64_t grid_all = grid;
+#if OMEGA_BATCH_EXTRAS
   bp.tpm_wg = -1;
+#endif
   if (tpm) {
+#if OMEGA_BATCH_EXTRAS
     sp.tp_done = c->d_kw_done + 3;
     c->tp_issued += (unsigned)n;
     bp.tpm_wg = (int)grid;
@@ -996,6 +999,7 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
     bp.poll_limit = c->poll_limit;
     bp.err_word = c->d_err;
     grid_all = grid + 1;
+#endif
   }
   if (join) {
     sp.tp_done = c->d_kw_done + 3;
@@ -1012,12 +1016,14 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
       c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);
     }
     c->wg_issued += (unsigned)grid;
+#if OMEGA_BATCH_EXTRAS
     bp.wg_done = c->d_kw_done + 4;
     bp.wg_target = c->wg_issued;
     bp.join_ctr = c->d_kw_done + 1;
     bp.join_target = c->q_issued;
     bp.poll_limit = c->poll_limit;
     bp.err_word = c->d_err;
+#endif
   }
   {
     hipError_t le = hipSuccess;

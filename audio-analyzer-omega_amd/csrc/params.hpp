@@ -250,12 +250,21 @@ struct MultiPlan {
 //       the roles of a frame land on one XCD (blockIdx % 8) and a CU sees the roles mixed
 //   [seg_begin[2], ...)  the resolutions of at most 8192 points (multi; wg_begin relative to seg_begin[2])
 // The K-weighting role counts itself into KWeightParams::kw_done when that is set.
+// the rejected meter-scheduling experiments inside batch_kernel (the join, the true-peak meter role:
+// capi.cpp omega_ctx::batch_join / tp_meter_in_batch) are compiled in only with OMEGA_BATCH_EXTRAS=1,
+// so that the product kernel carries neither their branches nor their kernel-argument bytes
+#ifndef OMEGA_BATCH_EXTRAS
+#define OMEGA_BATCH_EXTRAS 0
+#endif
+constexpr bool kBatchExtras = OMEGA_BATCH_EXTRAS != 0;
+
 struct BatchPlan {
   int seg_begin[3];
   int n_roles[2];
   int roles[2][3];
   int mr_res;
   MultiPlan multi;
+#if OMEGA_BATCH_EXTRAS
   // the join (omega_ctx::batch_join): every workgroup counts itself into wg_done when it is finished;
   // the one that completes the count (wg_target) does not finish before (int)(*join_ctr - join_target)
   // >= 0 (the side stream's meter queries), bounded by poll_limit, expiry -> err_word[1]
@@ -273,6 +282,7 @@ struct BatchPlan {
   int tpm_wg;
   unsigned tp_target;
   MeterPrepParams mq;
+#endif
 };
 
 // Fused spectrum analysis (cfg3): windowed rfft magnitude (A13) -> log-band max (A10) and raw

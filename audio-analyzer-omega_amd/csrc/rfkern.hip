@@ -643,6 +643,7 @@ void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
   kw_count_in(kp, tid);
 }
 
+#if OMEGA_BATCH_EXTRAS
 // bounded poll of one lane: (int)(*ctr - target) >= 0, expiry -> err_word[1]
 __device__ __forceinline__ void batch_wait(const unsigned* ctr, unsigned target, int limit, unsigned* err) {
   bool met = false;
@@ -690,13 +691,17 @@ __device__ __forceinline__ void batch_tp_meter(const SpectralParams& sp, const B
   }
 }
 
+#endif
+
 __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, char* smem) {
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
+#if OMEGA_BATCH_EXTRAS
   if (b == bp.tpm_wg) {
     batch_tp_meter(sp, bp, tid, smem);
     return;
   }
+#endif
   if (b < bp.seg_begin[2]) {
     const int sg = b < bp.seg_begin[1] ? 0 : 1;
     const int j = b - bp.seg_begin[sg], nr = bp.n_roles[sg];
@@ -732,6 +737,7 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
 __global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams sp, KWeightParams kp, BatchPlan bp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   batch_body(sp, kp, bp, smem);
+#if OMEGA_BATCH_EXTRAS
   if (bp.wg_done) {
     // the join: the workgroup that finishes the launch's count waits for the side stream's meter
     // queries, so this stream completes after them (no stream event, no kernel after the batch)
@@ -753,6 +759,7 @@ __global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams 
       }
     }
   }
+#endif
 }
 
 hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s) {
