@@ -14,7 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <map>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -249,7 +251,7 @@ struct omega_ctx {
     hipGraphExec_t exec;
   };
   std::vector<GraphEntry> graphs;
-  std::string err;
+  char err[512] = {};  // omega_last_error (a fixed buffer: reporting an error allocates nothing)
   // tables
   float2* d_tw[kMaxLog2] = {};
   float4* d_rtw1[2] = {};  // register-FFT twiddle tables (build_rf_twiddles), K = 4096 / 8192
@@ -353,7 +355,7 @@ int fail(omega_ctx* c, int code, const char* fmt, ...) {
   va_start(ap, fmt);
   std::vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
-  if (c) c->err = buf;
+  if (c) std::memcpy(c->err, buf, sizeof buf);
   return code;
 }
 
@@ -362,6 +364,21 @@ int fail(omega_ctx* c, int code, const char* fmt, ...) {
     hipError_t e_ = (x);                                                                       \
     if (e_ != hipSuccess) return fail(ctx, OMEGA_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
   } while (0)
+
+// The ABI contract (omega.h: no C++ exception and no abort crosses it): every extern "C" entry point
+// is a function-try-block whose handler maps what escaped -- std::bad_alloc from a host container, or
+// anything else -- to a status code and omega_last_error. Called only from inside a catch clause.
+int guard_fail(omega_ctx* c) noexcept {
+  try {
+    throw;
+  } catch (const std::bad_alloc&) {
+    return fail(c, OMEGA_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(c, OMEGA_EHIP, "internal error: %s", e.what());
+  } catch (...) {
+    return fail(c, OMEGA_EHIP, "internal error: unknown exception");
+  }
+}
 
 template <class T>
 int dalloc(omega_ctx* c, T** p, size_t count) {
@@ -374,13 +391,16 @@ int dalloc(omega_ctx* c, T** p, size_t count) {
 }
 
 // A per-call scratch buffer of at least `need` elements: grown by replacement (the old buffer freed
-// once the device is idle -- work already enqueued may still read it), so repeated calls with growing
-// sizes keep one buffer instead of accumulating them until omega_destroy.
+// once this context's streams are idle -- work already enqueued may still read it; other contexts and
+// streams on the device are not waited for), so repeated calls with growing sizes keep one buffer
+// instead of accumulating them until omega_destroy.
 template <class T>
 int grow(omega_ctx* c, T** p, int64_t* cap, int64_t need) {
   if (need <= *cap) return 0;
   if (*p) {
-    HIPC(c, hipDeviceSynchronize());
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (hipStream_t f : c->fork)
+      if (f) HIPC(c, hipStreamSynchronize(f));
     auto it = std::find(c->allocs.begin(), c->allocs.end(), static_cast<void*>(*p));
     if (it != c->allocs.end()) c->allocs.erase(it);
     (void)hipFree(*p);
@@ -1153,7 +1173,7 @@ extern "C" {
 
 const char* omega_version(void) { return "omega-mi355x 0.1 (gfx950, ABI 1)"; }
 
-void omega_config_default(omega_config* cfg) {
+void omega_config_default(omega_config* cfg) try {
   std::memset(cfg, 0, sizeof *cfg);
   cfg->sample_rate = 48000;
   cfg->max_freq = 20000;
@@ -1172,9 +1192,10 @@ void omega_config_default(omega_config* cfg) {
   cfg->short_len = 180;
   cfg->integrated_len = 3600;
   cfg->peak_len = 60;
+} catch (...) {
 }
 
-int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
+int omega_create(const omega_config* cfg, int device, omega_ctx** out) try {
   if (!cfg || !out) return OMEGA_EINVAL;
   *out = nullptr;
   omega_ctx* c = new (std::nothrow) omega_ctx();
@@ -1235,9 +1256,11 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) {
   if (!e) e = build_meter_state(c);
   *out = c;
   return e;
+} catch (...) {
+  return guard_fail(out ? *out : nullptr);
 }
 
-int omega_vu_reset(omega_ctx* c) {
+int omega_vu_reset(omega_ctx* c) try {
   if (!c) return OMEGA_EINVAL;
   c->vu_total = 0;
   if (!c->d_vu_st[0]) return 0;
@@ -1253,10 +1276,12 @@ int omega_vu_reset(omega_ctx* c) {
     HIPC(c, hipMemcpyAsync(c->d_vu_st[b], st.data(), st.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 int omega_vu_update(omega_ctx* c, const void* x, int32_t f64, int64_t n_updates, int32_t chunk, int64_t update_stride,
-                    int64_t channel_stride, const double* dt, double* out, int mem) {
+                    int64_t channel_stride, const double* dt, double* out, int mem) try {
   if (!c || !out || !dt) return OMEGA_EINVAL;
   if (!x || n_updates < 0 || chunk < 1) return fail(c, OMEGA_EINVAL, "vu update: bad input layout");
   if (n_updates == 0) return 0;
@@ -1307,6 +1332,8 @@ int omega_vu_update(omega_ctx* c, const void* x, int32_t f64, int64_t n_updates,
   c->vu_total += n_updates * chunk;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 // Savitzky-Golay (21, 3) weights of scipy.signal.savgol_filter's 'interp' mode: the least-squares
@@ -1353,7 +1380,7 @@ static void savgol_21_3(double W[21][21]) {
 }
 
 int omega_transients(omega_ctx* c, const void* x, int32_t f64, int64_t n_frames, int32_t n, int64_t frame_stride,
-                     double* out, int mem) {
+                     double* out, int mem) try {
   if (!c || !out) return OMEGA_EINVAL;
   if (!x || n_frames < 0 || frame_stride < n) return fail(c, OMEGA_EINVAL, "transients: bad frame layout");
   if (n < 64) return fail(c, OMEGA_EINVAL, "transients: frame length %d below 64 (transient.py:21)", n);
@@ -1431,9 +1458,11 @@ int omega_transients(omega_ctx* c, const void* x, int32_t f64, int64_t n_frames,
   }
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
-int omega_drum_reset(omega_ctx* c) {
+int omega_drum_reset(omega_ctx* c) try {
   if (!c) return OMEGA_EINVAL;
   if (!c->drum_bins) return 0;
   HIPC(c, hipSetDevice(c->device));
@@ -1443,10 +1472,12 @@ int omega_drum_reset(omega_ctx* c) {
   }
   HIPC(c, hipStreamSynchronize(c->stream));
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 int omega_drum_features(omega_ctx* c, const float* mag, int64_t n_frames, int32_t n_bins, int64_t mag_stride,
-                        double sensitivity, double* out, int mem) {
+                        double sensitivity, double* out, int mem) try {
   if (!c || !out) return OMEGA_EINVAL;
   if (!mag || n_frames < 0 || n_bins < 2 || mag_stride < n_bins)
     return fail(c, OMEGA_EINVAL, "drum features: bad magnitude layout (n_bins %d, stride %lld)", n_bins,
@@ -1512,13 +1543,15 @@ int omega_drum_features(omega_ctx* c, const float* mag, int64_t n_frames, int32_
   c->drum_cur = b;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, const uint8_t* bass,
                          const float* comp_instr, const float* comp_vocal, const float* vocal_sup,
                          const int32_t* ranges, int32_t p_lo, int32_t p_hi, float p_gamma,
-                         const int32_t* band_start, const int32_t* band_end, const float* band_smooth,
-                         int32_t n_bands) {
+                         const int32_t* band_start, const int32_t* band_end, const double* band_smooth,
+                         int32_t n_bands) try {
   if (!c) return OMEGA_EINVAL;
   if (n_bins < 1 || n_bins > kPostMaxBins || n_bands < 0 || n_bands > kPostMaxBands || !curve || !bass ||
       !comp_instr || !comp_vocal || !vocal_sup || !ranges || (n_bands && (!band_start || !band_end || !band_smooth)))
@@ -1529,6 +1562,12 @@ int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, cons
     if (band_start[b] < 0 || band_start[b] >= n_bins || band_end[b] > n_bins || band_end[b] < band_start[b])
       return fail(c, OMEGA_EINVAL, "post configure: band %d [%d, %d) outside %d bins", b, band_start[b],
                   band_end[b], n_bins);
+  std::vector<EmaCoef> coef((size_t)n_bands);
+  for (int b = 0; b < n_bands; ++b) {
+    const double f = band_smooth[b];
+    if (!(f >= 0.0 && f <= 1.0)) return fail(c, OMEGA_EINVAL, "post configure: band %d smoothing factor %g outside [0, 1]", b, f);
+    coef[b] = EmaCoef{f, 1.0 - f, (float)f, (float)(1.0 - f)};
+  }
   HIPC(c, hipSetDevice(c->device));
   PostParams p{};
   p.T = n_bins;
@@ -1550,7 +1589,8 @@ int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, cons
   };
   double* dc = nullptr;
   unsigned char* db = nullptr;
-  float *d0 = nullptr, *d1 = nullptr, *dv = nullptr, *dsf = nullptr;
+  float *d0 = nullptr, *d1 = nullptr, *dv = nullptr;
+  EmaCoef* dsf = nullptr;
   int *dbs = nullptr, *dbe = nullptr;
   int e = up(&dc, curve, (size_t)n_bins);
   if (!e) e = up(&db, bass, (size_t)n_bins);
@@ -1559,12 +1599,12 @@ int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, cons
   if (!e) e = up(&dv, vocal_sup, (size_t)n_bins);
   if (!e) e = up(&dbs, band_start, (size_t)n_bands);
   if (!e) e = up(&dbe, band_end, (size_t)n_bands);
-  if (!e) e = up(&dsf, band_smooth, (size_t)n_bands * 2);
+  if (!e) e = up(&dsf, coef.data(), (size_t)n_bands);
   if (!e) e = dalloc(c, &p.prev, (size_t)std::max(n_bands, 1) * 2);  // two EMA state buffers
-  if (!e) e = dalloc(c, &p.has_prev, 2);
+  if (!e) e = dalloc(c, &p.has_prev, 4);
   if (e) return e;
   p.prev_out = p.prev + std::max(n_bands, 1);
-  p.has_prev_out = p.has_prev + 1;
+  p.has_prev_out = p.has_prev + 2;
   p.curve = dc;
   p.bass = db;
   p.comp[0] = d0;
@@ -1575,19 +1615,23 @@ int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, cons
   p.sf = dsf;
   c->post = p;
   return omega_post_reset(c);
+} catch (...) {
+  return guard_fail(c);
 }
 
-int omega_post_reset(omega_ctx* c) {
+int omega_post_reset(omega_ctx* c) try {
   if (!c) return OMEGA_EINVAL;
   if (!c->post.T) return 0;
   HIPC(c, hipSetDevice(c->device));
-  HIPC(c, hipMemsetAsync(std::min(c->post.has_prev, c->post.has_prev_out), 0, 2 * sizeof(int), c->stream));
+  HIPC(c, hipMemsetAsync(std::min(c->post.has_prev, c->post.has_prev_out), 0, 4 * sizeof(int), c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int64_t stride, int32_t flags,
-                       float bass_boost, float* spectrum_out, float* bands_out, int32_t* content_out) {
+                       float bass_boost, float* spectrum_out, double* bands_out, int32_t* content_out) try {
   if (!c) return OMEGA_EINVAL;
   if (!c->post.T) return fail(c, OMEGA_EINVAL, "post process: omega_post_configure first");
   if (n_frames < 0 || stride < c->post.T || !spectra || !spectrum_out || (c->post.nb && !bands_out) ||
@@ -1605,15 +1649,20 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   p.spec_out = spectrum_out;
   p.band_out = bands_out;
   p.content_out = content_out;
-  if (c->post.nb)  // (+ the EMA's spare rows: post.hip post_ema_kernel)
-    if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, (n_frames + kEmaSpareRows) * c->post.nb)) return e;
+  if (c->post.nb) {  // (+ the EMA's spare rows: post.hip post_ema_kernel)
+    if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, (n_frames + kEmaSpareRows) * (c->post.nb + 1))) return e;
+  }
   p.band_raw = c->d_post_raw;
+  // the per-frame dtype flags after the raw band rows
+  p.frame64 = reinterpret_cast<int*>(c->d_post_raw + (n_frames + kEmaSpareRows) * c->post.nb);
   HIPC(c, launch_post(p, c->stream));
   if (c->post.nb) {  // the EMA wrote the other state buffer: it is the next call's input
     std::swap(c->post.prev, c->post.prev_out);
     std::swap(c->post.has_prev, c->post.has_prev_out);
   }
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 // A device-side ordering wait that expired (meters.hip: the prep kernel's wait for the batch's
@@ -1631,7 +1680,7 @@ int check_device_err(omega_ctx* c) {
               join ? "caller's stream joining the LUFS meters" : "");
 }
 
-void omega_destroy(omega_ctx* c) {
+void omega_destroy(omega_ctx* c) try {
   if (!c) return;
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->own) (void)hipStreamSynchronize(c->own);
@@ -1652,14 +1701,17 @@ void omega_destroy(omega_ctx* c) {
     if (ev) (void)hipEventDestroy(ev);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
+} catch (...) {
 }
 
-const char* omega_last_error(const omega_ctx* c) { return c ? c->err.c_str() : "null context"; }
+const char* omega_last_error(const omega_ctx* c) { return c ? c->err : "null context"; }
 
-int omega_set_stream(omega_ctx* c, void* s) {
+int omega_set_stream(omega_ctx* c, void* s) try {
   if (!c) return OMEGA_EINVAL;
   c->stream = static_cast<hipStream_t>(s);  // NULL = the null (default) stream, e.g. torch's default
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 void* omega_get_stream(const omega_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
@@ -1671,7 +1723,7 @@ int omega_get_config(const omega_ctx* c, omega_config* cfg, int* device) {
   return 0;
 }
 
-int omega_set_graphs(omega_ctx* c, int enable) {
+int omega_set_graphs(omega_ctx* c, int enable) try {
   if (!c) return OMEGA_EINVAL;
   c->use_graph = (enable & 1) != 0;
   // bits 1-2: 0 default (one batch launch where eligible, else 3), 1 sequential, 2 concurrent
@@ -1680,15 +1732,19 @@ int omega_set_graphs(omega_ctx* c, int enable) {
   c->layout = lay == 1 ? 0 : (lay == 2 ? 1 : (lay == 3 ? 2 : 3));
   drop_graphs(c);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
-int omega_synchronize(omega_ctx* c) {
+int omega_synchronize(omega_ctx* c) try {
   if (!c) return OMEGA_EINVAL;
   HIPC(c, hipStreamSynchronize(c->stream));
   return check_device_err(c);
+} catch (...) {
+  return guard_fail(c);
 }
 
-int omega_meter_reset(omega_ctx* c) {
+int omega_meter_reset(omega_ctx* c) try {
   if (!c) return OMEGA_EINVAL;
   const int C = c->cfg.n_channels;
   for (int b = 0; b < 2; ++b) {
@@ -1699,10 +1755,12 @@ int omega_meter_reset(omega_ctx* c) {
   }
   HIPC(c, hipStreamSynchronize(c->stream));
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t frame_stride, int64_t channel_stride,
-                         const omega_outputs* out, int mem) {
+                         const omega_outputs* out, int mem) try {
   if (!c || !out) return OMEGA_EINVAL;
   if (!x || n_frames < 0) return fail(c, OMEGA_EINVAL, "null input or negative frame count");
   if (int e = check_device_err(c)) return e;
@@ -1810,10 +1868,12 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
   if (e) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 int omega_process_stream(omega_ctx* c, const float* x, int64_t n_samples, int32_t hop, int64_t channel_stride,
-                         const omega_outputs* out, int mem, int64_t* n_frames_out) {
+                         const omega_outputs* out, int mem, int64_t* n_frames_out) try {
   if (!c) return OMEGA_EINVAL;
   if (n_frames_out) *n_frames_out = 0;
   if (hop < 1 || n_samples < 0) return fail(c, OMEGA_EINVAL, "hop must be >= 1 and n_samples >= 0");
@@ -1821,9 +1881,11 @@ int omega_process_stream(omega_ctx* c, const float* x, int64_t n_samples, int32_
   const int64_t nf = n_samples < W ? 0 : (n_samples - W) / hop + 1;
   if (n_frames_out) *n_frames_out = nf;
   return omega_process_frames(c, x, nf, hop, channel_stride, out, mem);
+} catch (...) {
+  return guard_fail(c);
 }
 
-int omega_combine(omega_ctx* c, const float* const* mags, int64_t n_cf, float* out, int mem) {
+int omega_combine(omega_ctx* c, const float* const* mags, int64_t n_cf, float* out, int mem) try {
   if (!c || !mags || !out) return OMEGA_EINVAL;
   if (n_cf <= 0) return n_cf == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
   HIPC(c, hipSetDevice(c->device));
@@ -1858,10 +1920,14 @@ int omega_combine(omega_ctx* c, const float* const* mags, int64_t n_cf, float* o
   HIPC(c, launch_combine(p, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
-int omega_true_peak(omega_ctx* c, const float* x, int64_t n, int32_t m, float* out_db, int mem) {
+int omega_true_peak(omega_ctx* c, const float* x, int64_t n, int32_t m, float* out_db, int mem) try {
   return omega_true_peak_os(c, x, n, m, 4, out_db, mem);
+} catch (...) {
+  return guard_fail(c);
 }
 
 // Plan of the any-length transform: radices (4s, then 2, 3, 5, 7, then the remaining primes) and the
@@ -1922,7 +1988,7 @@ int run_any(omega_ctx* c, AnyFftParams p, int truepeak) {
 }
 
 int omega_true_peak_os(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t oversampling, float* out_db,
-                       int mem) {
+                       int mem) try {
   if (!c || !x || !out_db) return OMEGA_EINVAL;
   if (oversampling != 1 && oversampling != 2 && oversampling != 4)
     return fail(c, OMEGA_EUNSUP, "true peak: oversampling %d unsupported (1, 2, 4)", oversampling);
@@ -1970,11 +2036,13 @@ int omega_true_peak_os(omega_ctx* c, const float* x, int64_t n, int32_t m, int32
   HIPC(c, tp_launch(c, m, sp, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 // the batch kernel's float32 K-weighting (kweight_kernel) on its own, for power-of-two frames
 int omega_k_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, float* weighted, float* lufs_inst,
-                      int mem) {
+                      int mem) try {
   if (!c || !x) return OMEGA_EINVAL;
   if (!is_pow2_in(m, 512, 16384)) return fail(c, OMEGA_EUNSUP, "k-weighting: frame length %d unsupported", m);
   if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
@@ -1996,6 +2064,8 @@ int omega_k_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, float*
   HIPC(c, launch_kweight(m, kp, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 // The float64 filter cascade of a weighting mode for the context's sample rate
@@ -2039,7 +2109,7 @@ int get_w64_stages(omega_ctx* c, int mode, W64Stage** out) {
 }
 
 int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t mode, float* weighted,
-                    float* lufs_inst, int mem) {
+                    float* lufs_inst, int mem) try {
   if (!c || !x) return OMEGA_EINVAL;
   if (mode < OMEGA_WEIGHT_K || mode > OMEGA_WEIGHT_Z) return fail(c, OMEGA_EINVAL, "weighting mode %d", mode);
   // scipy's filtfilt needs more samples than its padlen (9 for the first section of K, A and C)
@@ -2079,10 +2149,12 @@ int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t 
   }
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db, int64_t n_frames, double* meters,
-                       int mem) {
+                       int mem) try {
   if (!c || !lufs_inst || !tp_db || !meters) return OMEGA_EINVAL;
   if (n_frames <= 0) return n_frames == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
   if (int e = check_device_err(c)) return e;
@@ -2103,10 +2175,12 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
   if (e) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 int omega_bands_create(omega_ctx* c, int op, const int32_t* starts, const int32_t* ends, int32_t n_bands,
-                       int32_t n_out, const double* scale, const double* bin_scale, int32_t n_bins, omega_bands** out) {
+                       int32_t n_out, const double* scale, const double* bin_scale, int32_t n_bins, omega_bands** out) try {
   if (!c || !starts || !ends || !out || n_bands < 0 || n_out < 0 || n_bins <= 0) return OMEGA_EINVAL;
   if (op != OMEGA_BANDS_MAX && op != OMEGA_BANDS_MEAN) return fail(c, OMEGA_EINVAL, "unknown band op %d", op);
   HIPC(c, hipSetDevice(c->device));
@@ -2152,12 +2226,14 @@ int omega_bands_create(omega_ctx* c, int op, const int32_t* starts, const int32_
   }
   *out = b;
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 void omega_bands_destroy(omega_bands* b) { delete b; }  // device tables are owned by the context
 
 int omega_bands_apply(omega_ctx* c, omega_bands* b, const float* spec, int64_t n, int64_t spec_stride, float* out,
-                      int mem) {
+                      int mem) try {
   if (!c || !b || !spec || !out) return OMEGA_EINVAL;
   if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
   HIPC(c, hipSetDevice(c->device));
@@ -2175,9 +2251,11 @@ int omega_bands_apply(omega_ctx* c, omega_bands* b, const float* spec, int64_t n
   HIPC(c, launch_bands(p, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
-int omega_chroma(omega_ctx* c, const float* spec, int64_t n, int32_t n_bins, double df, double* out_raw, int mem) {
+int omega_chroma(omega_ctx* c, const float* spec, int64_t n, int32_t n_bins, double df, double* out_raw, int mem) try {
   if (!c || !spec || !out_raw || n_bins < 3 || !(df > 0)) return OMEGA_EINVAL;
   if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
   HIPC(c, hipSetDevice(c->device));
@@ -2230,9 +2308,11 @@ int omega_chroma(omega_ctx* c, const float* spec, int64_t n, int32_t n_bins, dou
                         c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
-int omega_rfft(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t window, float* mag, float* cplx, int mem) {
+int omega_rfft(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t window, float* mag, float* cplx, int mem) try {
   if (!c || !x || (!mag && !cplx)) return OMEGA_EINVAL;
   if (m < 1) return fail(c, OMEGA_EINVAL, "rfft: length %d", m);
   if (n <= 0) return n == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
@@ -2273,10 +2353,12 @@ int omega_rfft(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t windo
   HIPC(c, launch_rfft(m, p, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t window, omega_bands* bands,
-                  float* bands_out, double* chroma_out, float* mag_out, int mem) {
+                  float* bands_out, double* chroma_out, float* mag_out, int mem) try {
   if (!c || !x || (!bands_out && !chroma_out && !mag_out)) return OMEGA_EINVAL;
   if (m != 8192) return fail(c, OMEGA_EUNSUP, "spectra: frame length %d unsupported (8192)", m);
   if (bands_out && (!bands || bands->op != OMEGA_BANDS_MAX || bands->n_bins != m / 2 + 1 || bands->n_valid > 512))
@@ -2405,6 +2487,8 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
     HIPC(c, launch_spectra(m, p, grid, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
 }
 
 }  // extern "C"

@@ -8,10 +8,16 @@
 // Host side: the caller's bytes are memcpy'd into page-locked staging slots (the only host work);
 // a full slot is one batch of batch_hops * hop samples per channel. Per batch, on the ingest's copy
 // stream: one H2D of the raw interleaved bytes; on its compute stream (the context's stream): the gate
-// RMS per (channel, chunk), the gate state scan per channel, the unpack (carry of the previous
-// batch's last samples + convert + gate + gain, planar), omega_process_stream over the batch's frames,
-// and one D2H of the outputs into the slot's page-locked result block. The copy of batch b + 1
-// overlaps the analysis of batch b; the host never waits unless every staging slot is in flight.
+// RMS per capture chunk, the gate state scan, the unpack (carry of the previous batch's last samples +
+// convert + gate + gain, planar), omega_process_stream over the batch's frames, and one D2H of the
+// outputs into the slot's page-locked result block. The copy of batch b + 1 overlaps the analysis of
+// batch b; the host never waits unless every staging slot is in flight.
+//
+// The gate runs as the reference's capture loop does with any channel count: it reads chunk_size
+// samples of the interleaved stream at a time (capture.py:549-550: chunk_bytes = chunk_size * bytes
+// per sample, whatever the channels), so a chunk holds chunk_size / C frames (or straddles frames), one
+// RMS covers every channel of it, one background level and one silence counter (counting chunk_size
+// interleaved samples per chunk) serve all channels, and a gated chunk zeroes all its samples.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -40,18 +47,18 @@ struct IngestParams {
   int64_t pitch;
   float gain;
   int gate;                  // noise gate on
-  int chunk;                 // gate chunk (capture chunk_size)
-  int64_t n_chunks;          // n_new / chunk
-  float* rms;                // [C][n_chunks]
-  unsigned char* zero;       // [C][n_chunks] chunk gated to zeros
-  float* bg;                 // [C] background level (float32 after its first update, as numpy computes it)
-  int64_t* silence;          // [C] silence_samples
+  int chunk;                 // gate chunk (capture chunk_size), interleaved samples
+  int64_t n_chunks;          // n_new * C / chunk
+  float* rms;                // [n_chunks]
+  unsigned char* zero;       // [n_chunks] chunk gated to zeros
+  float* bg;                 // background level (float32 after its first update, as numpy computes it)
+  int64_t* silence;          // silence_samples
   float nf2, nf, one_m_alpha, alpha;  // float32(noise_floor * 2), float32(noise_floor), float32(1 - a), float32(a)
   int64_t silence_threshold;
 };
 
-__device__ __forceinline__ float ingest_sample(const IngestParams& p, int64_t i, int c) {
-  const int64_t k = i * p.C + c;
+// interleaved sample k = frame * C + channel
+__device__ __forceinline__ float ingest_sample(const IngestParams& p, int64_t k) {
   if (p.fmt == OMEGA_FMT_S16LE) {
     const short v = reinterpret_cast<const short*>(p.raw)[k];
     return (float)v / 32768.0f;  // astype(float32) / 32768.0 (capture.py:574)
@@ -59,27 +66,26 @@ __device__ __forceinline__ float ingest_sample(const IngestParams& p, int64_t i,
   return reinterpret_cast<const float*>(p.raw)[k];
 }
 
-// rms of one (chunk, channel): np.sqrt(np.mean(x ** 2)) in float32 (capture.py:623)
+// rms of one capture chunk (chunk_size interleaved samples): np.sqrt(np.mean(x ** 2)) in float32
+// (capture.py:623)
 __global__ __launch_bounds__(256) void ingest_rms_kernel(IngestParams p) {
   extern __shared__ float sq[];
-  const int c = blockIdx.y;
   const int64_t k = blockIdx.x;
   for (int i = threadIdx.x; i < p.chunk; i += 256) {
-    const float v = ingest_sample(p, k * p.chunk + i, c);
+    const float v = ingest_sample(p, k * p.chunk + i);
     sq[i] = v * v;
   }
   __syncthreads();
-  if (threadIdx.x == 0) p.rms[c * p.n_chunks + k] = __fsqrt_rn(np_mean_f32(sq, p.chunk));
+  if (threadIdx.x == 0) p.rms[k] = __fsqrt_rn(np_mean_f32(sq, p.chunk));
 }
 
-// the gate state machine of _process_audio_frame, chunk by chunk, one thread per channel
+// the gate state machine of _process_audio_frame, chunk by chunk (one thread: the stream's state)
 __global__ void ingest_gate_kernel(IngestParams p) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= p.C) return;
-  float bg = p.bg[c];
-  int64_t sil = p.silence[c];
+  if (threadIdx.x != 0) return;
+  float bg = *p.bg;
+  int64_t sil = *p.silence;
   for (int64_t k = 0; k < p.n_chunks; ++k) {
-    const float r = p.rms[c * p.n_chunks + k];
+    const float r = p.rms[k];
     // background_level = (1 - a) * bg + a * rms: Python floats times a float32 scalar stay float32
     if (r < p.nf2) bg = p.one_m_alpha * bg + p.alpha * r;
     const float b3 = bg * 3.0f;
@@ -91,10 +97,10 @@ __global__ void ingest_gate_kernel(IngestParams p) {
     } else {
       sil = 0;
     }
-    p.zero[c * p.n_chunks + k] = z;
+    p.zero[k] = z;
   }
-  p.bg[c] = bg;
-  p.silence[c] = sil;
+  *p.bg = bg;
+  *p.silence = sil;
 }
 
 // carry ++ gated, gain-scaled new samples, planar
@@ -106,9 +112,9 @@ __global__ __launch_bounds__(256) void ingest_unpack_kernel(IngestParams p) {
     if (i < p.carry) {
       v = p.prev[c * p.pitch + p.prev_off + i];
     } else {
-      const int64_t j = i - p.carry;
-      v = ingest_sample(p, j, c);
-      if (p.gate && p.zero[c * p.n_chunks + j / p.chunk]) v = 0.f;
+      const int64_t k = (i - p.carry) * p.C + c;
+      v = ingest_sample(p, k);
+      if (p.gate && p.zero[k / p.chunk]) v = 0.f;
       v = v * p.gain;  // audio_data * input_gain (omega4_main.py:660)
     }
     p.dst[c * p.pitch + i] = v;
@@ -159,7 +165,7 @@ struct omega_ingest {
   int64_t* d_sil = nullptr;
   int64_t max_chunks = 0;
   omega_ingest_stats st{};
-  std::string err;
+  char err[512] = {};  // omega_ingest_last_error (fixed: reporting an error allocates nothing)
 };
 
 namespace {
@@ -170,7 +176,7 @@ int ifail(omega_ingest* in, int code, const char* fmt, ...) {
   va_start(ap, fmt);
   std::vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
-  if (in) in->err = buf;
+  if (in) std::memcpy(in->err, buf, sizeof buf);
   return code;
 }
 
@@ -180,13 +186,28 @@ int ifail(omega_ingest* in, int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return ifail(in, OMEGA_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
   } while (0)
 
+// extern "C" entry points are function-try-blocks (the ABI contract, omega.h): what escapes becomes a
+// status code and omega_ingest_last_error. Called only from inside a catch clause.
+int iguard_fail(omega_ingest* in) noexcept {
+  try {
+    throw;
+  } catch (const std::bad_alloc&) {
+    return ifail(in, OMEGA_ENOMEM, "out of host memory");
+  } catch (const std::exception& e) {
+    return ifail(in, OMEGA_EHIP, "internal error: %s", e.what());
+  } catch (...) {
+    return ifail(in, OMEGA_EHIP, "internal error: unknown exception");
+  }
+}
+
 int ctx_call(omega_ingest* in, int code) {
   if (code) return ifail(in, code, "%s", omega_last_error(in->ctx));
   return 0;
 }
 
 int alloc_out(omega_ingest* in, omega_ingest::Out** out) {
-  auto* o = new omega_ingest::Out();
+  auto* o = new (std::nothrow) omega_ingest::Out();
+  if (!o) return ifail(in, OMEGA_ENOMEM, "result block: out of host memory");
   in->outs.push_back(o);
   const size_t rows = (size_t)in->B * in->C;
   IHIP(in, hipEventCreateWithFlags(&o->ev_done, hipEventDisableTiming));
@@ -255,7 +276,7 @@ int launch_slot(omega_ingest* in, int s, int64_t n_new) {
   p.gain = in->cfg.gain;
   p.gate = in->cfg.gate;
   p.chunk = in->cfg.chunk_size;
-  p.n_chunks = n_new / in->cfg.chunk_size;
+  p.n_chunks = n_new * in->C / in->cfg.chunk_size;
   p.rms = in->d_rms;
   p.zero = in->d_zero;
   p.bg = in->d_bg;
@@ -267,9 +288,9 @@ int launch_slot(omega_ingest* in, int s, int64_t n_new) {
   p.alpha = (float)a;
   p.silence_threshold = (int64_t)(in->cfg.sample_rate * in->cfg.silence_threshold_seconds);
   if (p.gate && p.n_chunks > 0) {
-    hipLaunchKernelGGL(ingest_rms_kernel, dim3((unsigned)p.n_chunks, (unsigned)in->C), dim3(256),
-                       (size_t)p.chunk * sizeof(float), in->comp, p);
-    hipLaunchKernelGGL(ingest_gate_kernel, dim3((in->C + 63) / 64), dim3(64), 0, in->comp, p);
+    hipLaunchKernelGGL(ingest_rms_kernel, dim3((unsigned)p.n_chunks), dim3(256), (size_t)p.chunk * sizeof(float),
+                       in->comp, p);
+    hipLaunchKernelGGL(ingest_gate_kernel, dim3(1), dim3(64), 0, in->comp, p);
   }
   const int64_t n = in->carry + n_new;
   const unsigned gx = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
@@ -321,7 +342,7 @@ int take_fill_slot(omega_ingest* in, int* out) {
 
 extern "C" {
 
-void omega_ingest_config_default(omega_ingest_config* c) {
+void omega_ingest_config_default(omega_ingest_config* c) try {
   if (!c) return;
   *c = omega_ingest_config{};
   c->format = OMEGA_FMT_F32LE;
@@ -337,15 +358,17 @@ void omega_ingest_config_default(omega_ingest_config* c) {
   c->silence_threshold_seconds = 0.25;
   c->background_alpha = 0.001;
   c->want = OMEGA_INGEST_COMBINED | OMEGA_INGEST_LUFS | OMEGA_INGEST_TRUE_PEAK | OMEGA_INGEST_METERS;
+} catch (...) {
 }
 
-int omega_ingest_create(omega_ctx* ctx, const omega_ingest_config* cfg, omega_ingest** out) {
+int omega_ingest_create(omega_ctx* ctx, const omega_ingest_config* cfg, omega_ingest** out) try {
   if (!ctx || !cfg || !out) return OMEGA_EINVAL;
   *out = nullptr;
   omega_config cc{};
   int device = 0;
   if (omega_get_config(ctx, &cc, &device)) return OMEGA_EINVAL;
-  auto* in = new omega_ingest();
+  auto* in = new (std::nothrow) omega_ingest();
+  if (!in) return OMEGA_ENOMEM;
   in->ctx = ctx;
   in->cfg = *cfg;
   in->C = cc.n_channels;
@@ -366,10 +389,11 @@ int omega_ingest_create(omega_ctx* ctx, const omega_ingest_config* cfg, omega_in
   if (in->B < 1 || cfg->ring_slots < 2) return bad("batch_hops >= 1 and ring_slots >= 2");
   if (cfg->chunk_size < 1 || cfg->chunk_size > 8192) return bad("chunk_size 1..8192 (capture.py:64)");
   in->slot_samples = (int64_t)in->B * in->H;
-  if (in->slot_samples % cfg->chunk_size) return bad("batch_hops * hop must be a multiple of chunk_size");
+  if (in->slot_samples * in->C % cfg->chunk_size)
+    return bad("batch_hops * hop * channels must be a multiple of chunk_size (whole capture chunks per batch)");
   in->slot_bytes = (size_t)in->slot_samples * in->C * in->bps;
   in->pitch = ((int64_t)in->W + in->slot_samples + 3) / 4 * 4;
-  in->max_chunks = in->slot_samples / cfg->chunk_size;
+  in->max_chunks = in->slot_samples * in->C / cfg->chunk_size;
   *out = in;
   IHIP(in, hipSetDevice(device));
   IHIP(in, hipStreamCreateWithFlags(&in->comp, hipStreamNonBlocking));
@@ -381,12 +405,12 @@ int omega_ingest_create(omega_ctx* ctx, const omega_ingest_config* cfg, omega_in
     IHIP(in, hipEventCreateWithFlags(&in->ev_unpacked[k], hipEventDisableTiming));
     IHIP(in, hipEventRecord(in->ev_unpacked[k], in->comp));
   }
-  IHIP(in, hipMalloc(&in->d_rms, (size_t)in->C * in->max_chunks * sizeof(float)));
-  IHIP(in, hipMalloc(&in->d_zero, (size_t)in->C * in->max_chunks));
-  IHIP(in, hipMalloc(&in->d_bg, in->C * sizeof(float)));
-  IHIP(in, hipMalloc(&in->d_sil, in->C * sizeof(int64_t)));
-  IHIP(in, hipMemset(in->d_bg, 0, in->C * sizeof(float)));
-  IHIP(in, hipMemset(in->d_sil, 0, in->C * sizeof(int64_t)));
+  IHIP(in, hipMalloc(&in->d_rms, (size_t)in->max_chunks * sizeof(float)));
+  IHIP(in, hipMalloc(&in->d_zero, (size_t)in->max_chunks));
+  IHIP(in, hipMalloc(&in->d_bg, sizeof(float)));
+  IHIP(in, hipMalloc(&in->d_sil, sizeof(int64_t)));
+  IHIP(in, hipMemset(in->d_bg, 0, sizeof(float)));
+  IHIP(in, hipMemset(in->d_sil, 0, sizeof(int64_t)));
   in->slots.resize(cfg->ring_slots);
   for (auto& sl : in->slots) {
     IHIP(in, hipHostMalloc(reinterpret_cast<void**>(&sl.h_raw), in->slot_bytes, hipHostMallocDefault));
@@ -395,9 +419,11 @@ int omega_ingest_create(omega_ctx* ctx, const omega_ingest_config* cfg, omega_in
   in->max_pending = std::max(cfg->max_pending_batches, 2);
   IHIP(in, hipStreamSynchronize(in->comp));
   return 0;
+} catch (...) {
+  return iguard_fail(out ? *out : nullptr);
 }
 
-int omega_ingest_push(omega_ingest* in, const void* bytes, int64_t n_bytes) {
+int omega_ingest_push(omega_ingest* in, const void* bytes, int64_t n_bytes) try {
   if (!in || (!bytes && n_bytes > 0) || n_bytes < 0) return OMEGA_EINVAL;
   IHIP(in, hipSetDevice(in->device));
   const unsigned char* b = static_cast<const unsigned char*>(bytes);
@@ -417,15 +443,24 @@ int omega_ingest_push(omega_ingest* in, const void* bytes, int64_t n_bytes) {
     }
   }
   return 0;
+} catch (...) {
+  return iguard_fail(in);
 }
 
-int omega_ingest_flush(omega_ingest* in) {
+int omega_ingest_flush(omega_ingest* in) try {
   if (!in) return OMEGA_EINVAL;
   IHIP(in, hipSetDevice(in->device));
   omega_ingest::Slot& sl = in->slots[in->fill_slot];
   if (sl.inflight || sl.fill == 0) return 0;
-  const size_t frame_bytes = (size_t)in->C * in->bps * in->cfg.chunk_size;
-  const size_t whole = sl.fill / frame_bytes * frame_bytes;
+  // whole frames that make whole capture chunks: a multiple of chunk / gcd(chunk, C) frames
+  int g = in->cfg.chunk_size, cc = in->C;
+  while (cc) {
+    const int r = g % cc;
+    g = cc;
+    cc = r;
+  }
+  const size_t unit = (size_t)in->C * in->bps * (size_t)(in->cfg.chunk_size / g);
+  const size_t whole = sl.fill / unit * unit;
   if (whole == 0) return 0;
   const size_t rest = sl.fill - whole;
   std::vector<unsigned char> tail(sl.h_raw + whole, sl.h_raw + sl.fill);
@@ -437,9 +472,11 @@ int omega_ingest_flush(omega_ingest* in) {
     return omega_ingest_push(in, tail.data(), (int64_t)rest);
   }
   return 0;
+} catch (...) {
+  return iguard_fail(in);
 }
 
-int omega_ingest_poll(omega_ingest* in, int64_t max_frames, const omega_outputs* out, int wait, int64_t* n_frames_out) {
+int omega_ingest_poll(omega_ingest* in, int64_t max_frames, const omega_outputs* out, int wait, int64_t* n_frames_out) try {
   if (!in || !out || max_frames < 0) return OMEGA_EINVAL;
   if (n_frames_out) *n_frames_out = 0;
   IHIP(in, hipSetDevice(in->device));
@@ -473,6 +510,8 @@ int omega_ingest_poll(omega_ingest* in, int64_t max_frames, const omega_outputs*
   if (n_frames_out) *n_frames_out = done;
   in->st.frames_polled += done;
   return 0;
+} catch (...) {
+  return iguard_fail(in);
 }
 
 int omega_ingest_get_stats(const omega_ingest* in, omega_ingest_stats* out) {
@@ -481,9 +520,9 @@ int omega_ingest_get_stats(const omega_ingest* in, omega_ingest_stats* out) {
   return 0;
 }
 
-const char* omega_ingest_last_error(const omega_ingest* in) { return in ? in->err.c_str() : "null ingest"; }
+const char* omega_ingest_last_error(const omega_ingest* in) { return in ? in->err : "null ingest"; }
 
-void omega_ingest_destroy(omega_ingest* in) {
+void omega_ingest_destroy(omega_ingest* in) try {
   if (!in) return;
   (void)hipSetDevice(in->device);
   if (in->comp) (void)hipStreamSynchronize(in->comp);
@@ -514,6 +553,7 @@ void omega_ingest_destroy(omega_ingest* in) {
   if (in->comp) (void)hipStreamDestroy(in->comp);
   if (in->copy) (void)hipStreamDestroy(in->copy);
   delete in;
+} catch (...) {
 }
 
 }  // extern "C"

@@ -325,6 +325,12 @@ constexpr int kDrumCols = 14;
 constexpr int kPostMaxBins = 2048;
 constexpr int kEmaSpareRows = 32;  // band_raw rows past the last frame (post_ema_kernel's unguarded block loads)
 constexpr int kPostMaxBands = 1024;
+// band EMA factor f (omega4_main.py:1044-1054: prev * f + v * (1 - f) with a Python float f): the
+// float64 forms (f, 1 - f) and the float32 forms numpy's weak-scalar promotion uses on float32 scalars
+struct EmaCoef {
+  double f, g;    // f, 1 - f
+  float f32, g32; // float32(f), float32(1 - f)
+};
 struct PostParams {
   const float* in;  // [n, stride] combined spectra
   int64_t n, stride;
@@ -338,17 +344,20 @@ struct PostParams {
   float p_g;
   const int* bs;               // [nb] band starts / ends
   const int* bend;
-  const float* sf;             // [nb] EMA factor
+  const EmaCoef* sf;           // [nb] EMA factor f in the forms the reference's numpy arithmetic uses
   int nb;
   int flags;                   // OMEGA_POST_* bits
   float bass_boost;
   float* spec_out;             // [n, T]
-  float* band_out;             // [n, nb]
+  double* band_out;            // [n, nb] (float32 values, or float64 on frames whose list held the int 1)
   float* band_raw;             // [n, nb] scratch: the clamped band values before the EMA
+  int* frame64;                // [n] scratch: 1 where a band clamped to the Python int 1 (float64 array)
   int* content_out;            // [n]
-  float* prev;                 // [nb] EMA state in (double-buffered: the kernels read one, write the other)
-  int* has_prev;
-  float* prev_out;             // [nb] EMA state out
+  // EMA state {value, float64 dtype, present} in (double-buffered: the kernels read one, write the
+  // other)
+  double* prev;                // [nb]
+  int* has_prev;               // [2]: present, float64 dtype
+  double* prev_out;            // [nb] EMA state out
   int* has_prev_out;
 };
 

@@ -17,7 +17,8 @@
 // percentile's lerp into an FMA (1 ulp off the reference value on the last golden frame, then every
 // bin of that frame).
 //   post_frame_kernel: one 256-thread workgroup per frame (independent frames).
-//   post_ema_kernel: one thread per band, the frames in order (the EMA recurrence), loads in blocks.
+//   post_ema_kernel + post_ema_fix_kernel: the band EMA in numpy's dtypes, warmed-up chunks checked
+//   and, where needed, re-run against the sequential recurrence.
 #include "stamps.hpp"
 
 namespace omega {
@@ -228,7 +229,11 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
   }
   OMEGA_STAMP(4);
   for (int i = t; i < T; i += kPostThreads) p.spec_out[f * T + i] = s[i];
-  // 6) band means -> sqrt -> clamp (before the EMA)
+  // 6) band means -> sqrt -> clamp (before the EMA). max(0, min(1, v)) returns the Python int 1 when
+  // sqrt(v) >= 1: the frame's band list then holds an int and np.array makes it float64 (:1034, :1037)
+  __shared__ int clamp_any;
+  if (t == 0) clamp_any = 0;
+  __syncthreads();
   for (int b = t; b < p.nb; b += kPostThreads) {
     const int lo = p.bs[b], hi = p.bend[b];
     float v;
@@ -237,23 +242,51 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
     } else {
       v = s[lo];
     }
-    if (v > 0.f) v = fminf(__fsqrt_rn(v), 1.0f);
+    if (v > 0.f) {
+      v = __fsqrt_rn(v);
+      if (!(v < 1.0f)) {
+        v = 1.0f;
+        clamp_any = 1;
+      }
+    }
     p.band_raw[f * p.nb + b] = v;
   }
+  __syncthreads();
+  if (t == 0 && p.nb > 0) p.frame64[f] = clamp_any;
   if (t == 0 && p.content_out) p.content_out[f] = content;
   OMEGA_STAMP(5);
 }
 
-// band_raw holds the clamped band values of the n frames; the EMA runs over them in frame order into
-// band_out.
+// The band EMA (omega4_main.py:1041-1056) over band_raw in frame order into band_out, with numpy's
+// types: the frame's band array is float32, or float64 when a band clamped to the int 1 (frame64);
+// prev_band_values keeps the previous array's dtype. Per band and frame, with P the previous value and
+// x this frame's raw value:
+//   a = P * f          in the previous array's dtype (f a weak Python float: float32(f) on float32)
+//   b = x * (1 - f)    in this array's dtype
+//   v = a + b          float64 if either is, stored into this frame's array (rounded to float32 there)
+// Every operation is rounded on its own (contraction off), so the device repeats numpy's results bit
+// for bit, denormals included (a decaying band sticks at the smallest denormal as it does on the CPU).
+struct EmaState {
+  double v;
+  bool f64;
+};
+__device__ __forceinline__ double ema_step(const EmaState& s, float x, bool x64, const EmaCoef& k) {
+  const double a = s.f64 ? s.v * k.f : (double)((float)s.v * k.f32);
+  if (s.f64 || x64) {
+    const double b = x64 ? (double)x * k.g : (double)(x * k.g32);
+    const double v = a + b;
+    return x64 ? v : (double)(float)v;
+  }
+  return (double)((float)a + x * k.g32);
+}
+
 // One thread per (band, chunk of kEmaChunk frames). The first chunk continues the stream's state; a
-// later chunk starts kEmaWarm frames early from that frame's value (as at a stream start) and runs
-// the same float32 recurrence up to its own frames: the warm-up's starting point contributes
-// sf^kEmaWarm <= 0.85^256 ~ 1e-18 of the value, far below float32 resolution, so the chunk joins the
-// sequential sequence bit for bit (a residual 1-ulp difference must survive ~200 roundings in a row;
-// tests/test_gpu_parity.py checks a 700-frame call against sequential calls bitwise).
-// Loads go in blocks of kEmaBlock frames (independent loads in flight; the recurrence is the only
-// dependence).
+// later chunk starts kEmaWarm frames early as at a stream start (no previous value) and runs the same
+// recurrence up to its own frames. Where the warm-up's start has faded out of every rounding (the usual
+// case) the chunk already holds the sequential values; post_ema_fix_kernel checks every chunk's first
+// value against the true state and re-runs the chunks where it differs (after a silence the true state
+// is still decaying while a warm-up from silent frames starts at 0). Loads go in blocks of kEmaBlock
+// frames, the next block's in flight during this block's recurrence.
 constexpr int kEmaBlock = 32;
 static_assert(kEmaBlock <= kEmaSpareRows, "the spare rows cover a block");
 constexpr int kEmaChunk = 64;
@@ -262,69 +295,118 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
   const int b = blockIdx.x * 64 + threadIdx.x;
   const int64_t c0 = (int64_t)blockIdx.y * kEmaChunk;
   if (b >= p.nb || c0 >= p.n) return;
-  const bool had = *p.has_prev != 0;
-  const float sf = p.sf[b], sf1 = p.sf[p.nb + b];  // float32(f), float32(1 - f)
+  const EmaCoef k = p.sf[b];
   const bool smooth = (p.flags & 8) != 0;
   const int64_t c1 = c0 + kEmaChunk < p.n ? c0 + kEmaChunk : p.n;
   const int64_t s0 = c0 == 0 ? 0 : (c0 > kEmaWarm ? c0 - kEmaWarm : 0);
   const bool exact_start = c0 == 0 || s0 == 0;
-  float prev = (exact_start && had) ? p.prev[b] : 0.f;
-  bool have = exact_start ? had : false;
+  const bool had = exact_start && p.has_prev[0] != 0;
+  EmaState st{had ? p.prev[b] : 0.0, had && p.has_prev[1] != 0};
+  bool have = had;
   // the row stride in a VGPR (opaque): the per-frame offsets are then vector arithmetic, instead of
   // 32 + 32 uniform 64-bit offsets the compiler would hold in (spilled) SGPRs
   int nb = p.nb;
   asm volatile("" : "+v"(nb));
   // blocks of kEmaBlock frames from s0: c0 - s0 is a multiple of the block (kEmaWarm and kEmaChunk
-  // are), so a block is all warm-up or all output. Loads are never guarded: band_raw has kEmaBlock
-  // spare rows past the last frame (values never stored); only the stream's last partial block guards
-  // its stores. The next block's loads are issued before this block's recurrence (double-buffered).
-  float v[kEmaBlock], nx[kEmaBlock];
-  auto load = [&](float (&d)[kEmaBlock], int64_t g0) {
+  // are), so a block is all warm-up or all output. Loads are never guarded: band_raw and frame64 have
+  // kEmaBlock spare rows past the last frame (values never used); only the stream's last partial
+  // block guards its stores.
+  float nx[kEmaBlock];
+  auto load = [&](int64_t g0) {
     const float* c = p.band_raw + g0 * nb + b;
 #pragma unroll
     for (int i = 0; i < kEmaBlock; ++i) {
-      d[i] = *c;
+      nx[i] = *c;
       c += nb;
     }
   };
-  load(nx, s0);
+  load(s0);
   for (int64_t f0 = s0; f0 < c1; f0 += kEmaBlock) {
+    float x[kEmaBlock];
 #pragma unroll
-    for (int i = 0; i < kEmaBlock; ++i) v[i] = nx[i];
-    if (f0 + kEmaBlock < c1) load(nx, f0 + kEmaBlock);
-    if (smooth) {
-      // frame 0 of the block: no previous value only at a stream's very start
-      if (have) v[0] = prev * sf + v[0] * sf1;
-#pragma unroll
-      for (int i = 1; i < kEmaBlock; ++i) v[i] = v[i - 1] * sf + v[i] * sf1;
-    }
-    have = true;
+    for (int i = 0; i < kEmaBlock; ++i) x[i] = nx[i];
+    if (f0 + kEmaBlock < c1) load(f0 + kEmaBlock);
     const int nf = c1 - f0 < kEmaBlock ? (int)(c1 - f0) : kEmaBlock;
-    prev = v[kEmaBlock - 1];
-    if (nf < kEmaBlock) {
+    double v[kEmaBlock];
 #pragma unroll
-      for (int i = 0; i < kEmaBlock - 1; ++i) prev = i == nf - 1 ? v[i] : prev;
+    for (int i = 0; i < kEmaBlock; ++i) {
+      const bool x64 = p.frame64[f0 + i] != 0;
+      v[i] = (smooth && have) ? ema_step(st, x[i], x64, k) : (double)x[i];
+      if (i < nf) st = EmaState{v[i], x64};
+      have = true;
     }
     if (f0 >= c0) {  // this chunk's frames (the warm-up frames belong to the chunk before)
-      float* o = p.band_out + f0 * nb + b;
-      if (nf == kEmaBlock) {
+      double* o = p.band_out + f0 * nb + b;
 #pragma unroll
-        for (int i = 0; i < kEmaBlock; ++i) {
-          *o = v[i];
-          o += nb;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < kEmaBlock; ++i) {
-          if (i < nf) *o = v[i];
-          o += nb;
-        }
+      for (int i = 0; i < kEmaBlock; ++i) {
+        if (i < nf) *o = v[i];
+        o += nb;
       }
     }
   }
-  if (c1 == p.n) {  // the state for the next call, in the other buffer (chunk 0 may still be reading)
-    p.prev_out[b] = prev;
-    if (b == 0) *p.has_prev_out = 1;
+}
+
+// One thread per band, after post_ema_kernel: the chunks in order, each one's first value checked
+// against the step from the true state (the end of the chunk before, after its own check); equal bits
+// mean the rest of the chunk is the sequential recurrence already (the same operations on the same
+// values), otherwise the chunk is re-run from the true state. Writes the stream state for the next
+// call. The common path waits on no load: each chunk's first raw value, flag and stored values are
+// loaded kFixAhead chunks ahead.
+constexpr int kFixAhead = 8;
+__global__ __launch_bounds__(64) void post_ema_fix_kernel(PostParams p) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= p.nb) return;
+  const EmaCoef k = p.sf[b];
+  const bool smooth = (p.flags & 8) != 0;
+  const int64_t n = p.n, nb = p.nb;
+  const int64_t nch = (n + kEmaChunk - 1) / kEmaChunk;
+  auto last_of = [&](int64_t ch) { return (ch + 1) * kEmaChunk < n ? (ch + 1) * kEmaChunk - 1 : n - 1; };
+  int64_t e0 = last_of(0);
+  EmaState st{p.band_out[e0 * nb + b], p.frame64[e0] != 0};
+  if (smooth) {
+    for (int64_t ch0 = 1; ch0 < nch; ch0 += kFixAhead) {
+      float x0[kFixAhead];
+      double v0[kFixAhead], ve[kFixAhead];
+      bool d0[kFixAhead], de[kFixAhead];
+#pragma unroll
+      for (int j = 0; j < kFixAhead; ++j) {
+        const int64_t ch = ch0 + j < nch ? ch0 + j : nch - 1;
+        const int64_t f = ch * kEmaChunk, e = last_of(ch);
+        x0[j] = p.band_raw[f * nb + b];
+        d0[j] = p.frame64[f] != 0;
+        v0[j] = p.band_out[f * nb + b];
+        ve[j] = p.band_out[e * nb + b];
+        de[j] = p.frame64[e] != 0;
+      }
+#pragma unroll
+      for (int j = 0; j < kFixAhead; ++j) {
+        const int64_t ch = ch0 + j;
+        if (ch >= nch) break;
+        const double v = ema_step(st, x0[j], d0[j], k);
+        if (__double_as_longlong(v) == __double_as_longlong(v0[j])) {
+          st = EmaState{ve[j], de[j]};
+          continue;
+        }
+        // re-run this chunk from the true state (its later chunks' checks use the values written here)
+        const int64_t f1 = last_of(ch);
+        int64_t f = ch * kEmaChunk;
+        p.band_out[f * nb + b] = v;
+        st = EmaState{v, d0[j]};
+        for (++f; f <= f1; ++f) {
+          const bool x64 = p.frame64[f] != 0;
+          const double w = ema_step(st, p.band_raw[f * nb + b], x64, k);
+          p.band_out[f * nb + b] = w;
+          st = EmaState{w, x64};
+        }
+      }
+    }
+  } else {
+    st = EmaState{p.band_out[(n - 1) * nb + b], p.frame64[n - 1] != 0};
+  }
+  p.prev_out[b] = st.v;
+  if (b == 0) {
+    p.has_prev_out[0] = 1;
+    p.has_prev_out[1] = st.f64 ? 1 : 0;
   }
 }
 
@@ -334,9 +416,11 @@ hipError_t launch_post(const PostParams& p, hipStream_t s) {
   if (p.T < 1 || p.T > kPostMaxBins || p.nb < 0 || p.nb > kPostMaxBands) return hipErrorInvalidValue;
   if (p.n == 0) return hipSuccess;
   hipLaunchKernelGGL(post_frame_kernel, dim3((unsigned)p.n), dim3(kPostThreads), 0, s, p);
-  if (p.nb > 0)
+  if (p.nb > 0) {
     hipLaunchKernelGGL(post_ema_kernel, dim3((p.nb + 63) / 64, (unsigned)((p.n + kEmaChunk - 1) / kEmaChunk)), dim3(64), 0,
                        s, p);
+    hipLaunchKernelGGL(post_ema_fix_kernel, dim3((p.nb + 63) / 64), dim3(64), 0, s, p);
+  }
   return hipGetLastError();
 }
 

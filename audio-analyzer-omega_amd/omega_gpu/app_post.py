@@ -45,9 +45,10 @@ def _band_table(fs, fft_base, bars, n_bins):
 
 class SpectrumPostProcessor:
     """One stream's post-processing of [F, T] combined spectra (T = bars, 512 in the app). Options are
-    the app's toggles (omega4_main.py:158-161, :343-346). ``process`` returns (spectrum [F, T],
-    band_values [F, n_bands], content [F]: indices into CONTENT_TYPES); the band EMA carries over
-    between calls (``reset`` starts a new stream)."""
+    the app's toggles (omega4_main.py:158-161, :343-346). ``process`` returns (spectrum [F, T] float32,
+    band_values [F, n_bands] float64 -- each row numpy's float32 or float64 band array exactly, see
+    omega.h --, content [F]: indices into CONTENT_TYPES); the band EMA carries over between calls
+    (``reset`` starts a new stream)."""
 
     def __init__(self, comb_frequencies, sample_rate: int = 48000, fft_size_base: int = 2048, bars: int = 512,
                  psychoacoustic_enabled: bool = True, psycho_bass_boost: float = 1.5,
@@ -88,7 +89,7 @@ class SpectrumPostProcessor:
         hi = min(lo + 1, T - 1)
         gamma = np.float32(vi - np.float32(lo))
         bs, be, sf = _band_table(sample_rate, fft_size_base, bars, T)
-        smooth = np.concatenate([sf.astype(np.float32), (1 - sf).astype(np.float32)])
+        smooth = np.ascontiguousarray(sf, np.float64)
         self.n_bands = len(bs)
         self._flags = ((PSYCHO if psychoacoustic_enabled else 0) | (FREQ_COMP if freq_compensation_enabled else 0)
                        | (NORMALIZE if normalization_enabled else 0) | (SMOOTH if smoothing_enabled else 0))
@@ -111,7 +112,7 @@ class SpectrumPostProcessor:
             raise ValueError(f"spectra must be [F, {self.n_bins}] float32 rows")
         F = x.shape[0]
         spec = torch.empty((F, self.n_bins), dtype=torch.float32, device=x.device)
-        bands = torch.empty((F, self.n_bands), dtype=torch.float32, device=x.device)
+        bands = torch.empty((F, self.n_bands), dtype=torch.float64, device=x.device)
         content = torch.empty(F, dtype=torch.int32, device=x.device)
         self._eng._bind_stream(x)
         self._eng._check(L.lib().omega_post_process(self._eng._ctx, x.data_ptr(), F, x.stride(0), self._flags,

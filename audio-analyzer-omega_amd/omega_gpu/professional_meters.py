@@ -50,10 +50,7 @@ class ProfessionalMetering:
         self.sample_rate = sample_rate
         self.gate_threshold = -70.0
         self.weighting_mode = "K"
-        hp_b, hp_a = _butter2_highpass(38.0, sample_rate)
-        sh_b, sh_a = _butter2_highpass(1500.0, sample_rate)
-        self.k_weighting_filter = {"hp_b": hp_b, "hp_a": hp_a, "shelf_b": sh_b, "shelf_a": sh_a,
-                                   "shelf_gain": 10 ** (4.0 / 20)}
+        self.k_weighting_filter = self.create_k_weighting_filter()
         self.current_lufs = {"momentary": -100.0, "short_term": -100.0, "integrated": -100.0, "range": 0.0,
                              "true_peak": -100.0}
         self.current_true_peak = -100.0
@@ -70,6 +67,15 @@ class ProfessionalMetering:
     def apply_k_weighting(self, audio_data: np.ndarray) -> np.ndarray:
         """professional_meters.py:129-153 (returned as float64 like scipy's filtfilt)."""
         return self._weighted(audio_data, "K")
+
+    def create_k_weighting_filter(self):
+        """professional_meters.py:48-72: second-order Butterworth high-passes at 38 Hz and at 1500 Hz
+        (the reference's "simplified shelf": iirfilter(2, ..., btype='high', ftype='butter')) and the
+        +4 dB shelf gain it computes but never applies (:59). The device builds the same coefficients
+        for the K-weighting it runs (omega_k_weighting / omega_weighting)."""
+        hp_b, hp_a = _butter2_highpass(38.0, self.sample_rate)
+        sh_b, sh_a = _butter2_highpass(1500.0, self.sample_rate)
+        return {"hp_b": hp_b, "hp_a": hp_a, "shelf_b": sh_b, "shelf_a": sh_a, "shelf_gain": 10 ** (4.0 / 20)}
 
     def create_a_weighting_filter(self):
         """professional_meters.py:74-107: the four cascaded Butterworth sections (the device builds the

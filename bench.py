@@ -255,26 +255,30 @@ def kernel_time_ms(eng, xd, reps=20):
     return s.elapsed_time(e) / reps, ncf
 
 
-def cfg3_line(dev, reps=20):
+def cfg3_line(dev, reps=20, n_batches=4):
     """BASELINE cfg3, the HBM-roofline run: 4096 mono frames x 8192 samples, fused windowed rfft ->
     512 log bands + 12-bin chromagram (omega_spectra), one launch per batch, inputs resident in HBM.
+    The launches rotate over n_batches distinct input batches (134 MB each: 4 x 134 MB = 537 MB, past
+    the 256 MiB Infinity Cache), so every launch reads its frames from HBM, not from on-die cache.
     Bytes per frame from SURVEY.md §8(d): 4 * 8192 in + 4 * (512 + 12) out = 34,864."""
     from omega_gpu import Engine, Resolution
     from omega_gpu import _lib as L
     from omega_gpu.engine import BandTable
     n, m = 4096, 8192
-    x = torch.from_numpy(cfg3_input(n, m)).to(dev)
+    x0 = torch.from_numpy(cfg3_input(n, m)).to(dev)
+    # distinct batches: the same frames scaled per batch (distinct bytes, same workload)
+    xs = [x0] + [x0 * (1.0 + 0.125 * k) for k in range(1, n_batches)]
     eng = Engine([Resolution((20, 20000), m, m // 4, 1.0)], FS, 20000, 512, device=dev.index or 0)
     st, en, comp = band_table_512()
     bt = BandTable(eng, L.BANDS_MAX, st, en, 512, m // 2 + 1, scale=comp)
     out = {"bands": torch.empty(n, 512, device=dev), "chroma": torch.empty(n, 12, dtype=torch.float64, device=dev)}
-    for _ in range(3):
-        eng.spectra(x, "hann", bands=bt, chroma=True, out=out)
+    for k in range(n_batches):
+        eng.spectra(xs[k], "hann", bands=bt, chroma=True, out=out)
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        eng.spectra(x, "hann", bands=bt, chroma=True, out=out)
+    for i in range(reps):
+        eng.spectra(xs[i % n_batches], "hann", bands=bt, chroma=True, out=out)
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / reps
@@ -283,9 +287,105 @@ def cfg3_line(dev, reps=20):
     traffic, src = kernel_traffic("cfg3")
     return {"workload": "cfg3: 4096 mono frames x 8192, Hann rfft -> 512 log bands (A10) + chromagram (A12), fused",
             "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_batch": ms,
+            "working_set": f"{n_batches} distinct input batches of {n * m * 4 / 1e6:.0f} MB rotated per launch "
+                           f"({n_batches * n * m * 4 / 2**20:.0f} MiB > the 256 MiB Infinity Cache)",
             "roofline": {"bound": "hbm", "kernel": "spectra_rf_kernel<4096>", "achieved": gbs, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": traffic, "traffic_source": src,
                          "bytes_per_frame": bpf, "algorithmic_bytes_per_launch": n * bpf}}
+
+
+PUBLISHED_MRFFT_MS = 0.20  # MultiResolutionFFT 0.20 ms per iteration (docs/MULTI_RESOLUTION_FFT_IMPROVEMENTS.md:193-195)
+
+
+def latency_line(dev, iters=1000, lufs_iters=300, cpu=True):
+    """The drop-in surfaces the app calls once per display frame, per-call latency on the host clock:
+    (a) benchmark_multi_fft (multi_resolution_fft.py:467-494: default configs, 512-sample chunks,
+    process_audio_chunk + combine_results_optimized per iteration) -- the reference's only published
+    on-path figure is 0.20 ms per iteration; (b) ProfessionalMetering.calculate_lufs at the app's shape
+    (omega4_main.py:1082: 2048-sample Hann-windowed float64 frames; professional_meters.py:231-281).
+    Beside each, the oracle's equivalent on this host (one core)."""
+    from omega_gpu.multi_resolution_fft import benchmark_multi_fft
+    from omega_gpu.professional_meters import ProfessionalMetering
+    mr = benchmark_multi_fft(FS, 512, iters, device=dev.index or 0)
+    rng = np.random.default_rng(8)
+    frames = [(0.3 * np.sin(2 * np.pi * 440 * np.arange(2048) / FS + 0.1 * k) + 0.01 * rng.standard_normal(2048))
+              * np.hanning(2048) for k in range(64)]
+    pm = ProfessionalMetering(FS, device=dev.index or 0)
+    for k in range(10):
+        pm.calculate_lufs(frames[k % 64])
+    t0 = time.perf_counter()
+    for k in range(lufs_iters):
+        pm.calculate_lufs(frames[k % 64])
+    lufs_ms = (time.perf_counter() - t0) / lufs_iters * 1e3
+    line = {"workload": "drop-in per-call latency: benchmark_multi_fft (default configs, 512-sample chunks, "
+                        "process_audio_chunk + combine_results_optimized) and calculate_lufs on 2048-sample Hann "
+                        "float64 frames (the app's per-display-frame calls), host clock",
+            "mrfft_ms_per_iteration": mr["avg_time_ms"], "mrfft_published_ms": PUBLISHED_MRFFT_MS,
+            "mrfft_vs_published": PUBLISHED_MRFFT_MS / mr["avg_time_ms"],
+            "calculate_lufs_ms_per_call": lufs_ms}
+    if cpu:
+        os.environ.setdefault("OMP_NUM_THREADS", "1")
+        from oracle import omega_ref as R
+        st = R.MRFFTStream()
+        x = np.random.random(512).astype(np.float32)
+        for _ in range(10):
+            st.process(x)
+        n = max(100, iters // 5)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            res = st.process(x)
+            if res:
+                R.combine(res)
+        line["mrfft_oracle_ms_per_iteration"] = (time.perf_counter() - t0) / n * 1e3
+        ms = R.MeterState(FS)
+        t0 = time.perf_counter()
+        for k in range(lufs_iters):
+            ms.update(frames[k % 64])
+        line["calculate_lufs_oracle_ms_per_call"] = (time.perf_counter() - t0) / lufs_iters * 1e3
+    return line
+
+
+def cfg1_line(dev, reps=20, cpu=True):
+    """BASELINE cfg1 (configs[0], the plumbing config): one 48 kHz mono stream, hop 512, W = 1024, one
+    1024-point resolution + combine(512), K-weighted LUFS + true peak + meters (momentary over 24
+    frames), 600 frames of 0.5 sin(2 pi 1000 t); the whole stream in one omega_process_stream call
+    (device-resident), beside the oracle's per-frame loop over the same 600 frames on one core."""
+    from omega_gpu import Engine, Resolution
+    W1, H1, F1 = 1024, 512, 600
+    n = W1 + H1 * (F1 - 1)
+    t = np.arange(n) / FS
+    x = (0.5 * np.sin(2 * np.pi * 1000 * t)).astype(np.float32)
+    xd = torch.from_numpy(x).to(dev)
+    eng = Engine([Resolution((20, 20000), W1, H1, 1.0)], FS, 20000, target_bins=T, frame_size=W1,
+                 device=dev.index or 0)
+    out = eng.process_stream(xd, n, H1, combined=True, meters=True)
+    for _ in range(3):
+        eng.process_stream(xd, n, H1, combined=True, meters=True, out=out)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        eng.process_stream(xd, n, H1, combined=True, meters=True, out=out)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / reps
+    line = {"workload": "cfg1: 48 kHz mono stream, hop 512, W 1024, one 1024-pt resolution + combine(512), K-LUFS + "
+                        "4x TP + meters (momentary over 24 frames), 600 frames of 0.5 sin(2 pi 1000 t), one call",
+            "value": F1 / (ms * 1e-3), "unit": "frames/s", "ms_per_call": ms, "frames": F1}
+    if cpu:
+        os.environ.setdefault("OMP_NUM_THREADS", "1")
+        from oracle import omega_ref as R
+        st = R.MeterState(FS)
+        cfgs = (R.FFTConfig((20, 20000), W1, H1, 1.0),)
+        t0 = time.perf_counter()
+        for f in range(F1):
+            fr = x[f * H1:f * H1 + W1]
+            _, _, li, tp = R.full_frame(fr, configs=cfgs, target_bins=T)
+            st.update(fr, li, tp)
+        dt = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": F1 / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+                                "sample": f"the same {F1} frames through the oracle's per-frame loop, {dt:.2f} s"}
+    return line
 
 
 def drums_line(dev, reps=20, n=4096, bins=1025):
@@ -335,7 +435,7 @@ def post_line(dev, reps=20, n=4096, bins=512):
     e.record()
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / reps
-    bpf = 4 * (2 * bins + pp.n_bands + 1)
+    bpf = 4 * (2 * bins + 1) + 8 * pp.n_bands
     gbs = n * bpf / (ms * 1e-3) / 1e9
     return {"workload": f"app post-processing: {n} consecutive combined spectra x {bins} bins of one stream "
                         f"({pp.n_bands} bands)",
@@ -603,6 +703,8 @@ def main(argv=None):
             line["cfg5"] = cfg5
         if world == 1 and not a.no_cfg3 and not standin:
             line["cfg3"] = cfg3_line(be.dev)
+            line["cfg1"] = cfg1_line(be.dev, cpu=not a.no_cpu_baseline)
+            line["latency"] = latency_line(be.dev, cpu=not a.no_cpu_baseline)
             line["drums"] = drums_line(be.dev)
             line["app_post"] = post_line(be.dev)
         print(json.dumps(line), flush=True)

@@ -158,7 +158,8 @@ int omega_combine(omega_ctx* ctx, const float* const* mags, int64_t n_cf, float*
 int omega_true_peak(omega_ctx* ctx, const float* x, int64_t n, int32_t m, float* out_db, int mem);
 /* calculate_true_peak(x, oversampling) (professional_meters.py:283-299) for oversampling 1, 2 or 4:
  * max |resample(x, oversampling * m)| over the phases n + p / oversampling; other factors return
- * OMEGA_EUNSUP. */
+ * OMEGA_EUNSUP. n frames of any length m >= 1, contiguous: powers of two 512..16384 on the
+ * register-FFT / Stockham kernels, every other length on the mixed-radix transform (anyfft.hip). */
 int omega_true_peak_os(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t oversampling, float* out_db,
                        int mem);
 
@@ -232,10 +233,15 @@ int omega_drum_reset(omega_ctx* ctx);
  * curve[T] equal-loudness by position, bass[T] (combine frequency < 250 Hz), comp_instr / comp_vocal
  * [T] compensation factors, vocal_sup[T], ranges {bass_end, vocal_start, vocal_end, high_start},
  * the percentile's sorted ranks and float32 gamma, bands [n_bands] (start, end) already truncated
- * as the reference's loop does, band_smooth[2 * n_bands] = float32(f), float32(1 - f).
+ * as the reference's loop does, band_smooth[n_bands] = the EMA factor f of each band (in [0, 1]).
  * omega_post_process (device memory only): n_frames spectra at row stride `stride` -> spectrum_out
- * [n, T], bands_out [n, n_bands] (after the EMA, which runs across frames in order and across calls),
- * content_out [n] (0 instrumental, 1 vocal, 2 bass-heavy; may be NULL). flags: OMEGA_POST_*. */
+ * [n, T] float32, bands_out [n, n_bands] float64 (after the EMA, which runs across frames in order and
+ * across calls), content_out [n] (0 instrumental, 1 vocal, 2 bass-heavy; may be NULL). flags:
+ * OMEGA_POST_*. Bands are numpy's values bit for bit: a frame's band list is float32, or float64 when
+ * a band clamps to the Python int 1 (:1034: max(0, min(1, v)) returns the int), and the EMA
+ * (:1041-1054) runs in the dtypes numpy gives each term -- bands_out holds both exactly. (A frame
+ * whose every band clamps would make numpy's array int64; after the 98th-percentile normalisation
+ * to 0.8 no frame reaches that.) */
 enum {
   OMEGA_POST_PSYCHO = 1,      /* equal-loudness curve + bass boost */
   OMEGA_POST_FREQ_COMP = 2,   /* apply_frequency_compensation */
@@ -245,10 +251,10 @@ enum {
 int omega_post_configure(omega_ctx* ctx, int32_t n_bins, const double* curve, const uint8_t* bass,
                          const float* comp_instr, const float* comp_vocal, const float* vocal_sup,
                          const int32_t* ranges, int32_t p_lo, int32_t p_hi, float p_gamma,
-                         const int32_t* band_start, const int32_t* band_end, const float* band_smooth,
+                         const int32_t* band_start, const int32_t* band_end, const double* band_smooth,
                          int32_t n_bands);
 int omega_post_process(omega_ctx* ctx, const float* spectra, int64_t n_frames, int64_t stride, int32_t flags,
-                       float bass_boost, float* spectrum_out, float* bands_out, int32_t* content_out);
+                       float bass_boost, float* spectrum_out, double* bands_out, int32_t* content_out);
 int omega_post_reset(omega_ctx* ctx);
 int omega_spectra(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_t window, omega_bands* bands,
                   float* bands_out, double* chroma_out, float* mag_out, int mem);
@@ -279,7 +285,12 @@ int omega_transients(omega_ctx* ctx, const void* x, int32_t f64, int64_t n_frame
  * of chunk_size samples, s16 scaled by 1/32768), its per-chunk noise gate (:620-641: RMS, background
  * EMA, silence counter -> zeros) and the app's input gain + ring buffer (omega4_main.py:648-688),
  * feeding omega_process_stream: frame f of every channel covers stream samples [f*hop, f*hop + W).
- * Bytes are interleaved over the context's n_channels. omega_ingest_push memcpy's them into
+ * Bytes are interleaved over the context's n_channels. The gate works as the reference's capture
+ * loop does for any channel count: a chunk is chunk_size interleaved samples (capture.py:549-550,
+ * chunk_size / C frames), one RMS over all its channels, one background level and one silence
+ * counter (+chunk_size per quiet chunk) for the stream, a gated chunk zeroes every channel of it.
+ * The gate's float32 arithmetic is numpy >= 2's (NEP 50: a Python float times a float32 scalar stays
+ * float32; the golden vectors were recorded with numpy 2.2.6). omega_ingest_push memcpy's them into
  * page-locked staging slots; each full slot (batch_hops * hop samples per channel) is copied to the
  * device on a copy stream and analysed on the ingest's compute stream (bound to the context with
  * omega_set_stream; destroy the ingest before the context, and before using the context directly
@@ -294,7 +305,7 @@ typedef struct {
   int32_t format;                   /* omega_sample_format */
   int32_t sample_rate;              /* for the gate's silence threshold (capture.py:227) */
   int32_t hop;                      /* frame hop H, multiple of 4 */
-  int32_t batch_hops;               /* hops per device batch; batch_hops * hop % chunk_size == 0 */
+  int32_t batch_hops;               /* hops per device batch; batch_hops * hop * n_channels % chunk_size == 0 */
   int32_t ring_slots;               /* page-locked input staging slots, >= 2 */
   int32_t max_pending_batches;      /* result blocks kept until polled (>= 2); beyond, the oldest drop */
   int32_t chunk_size;               /* capture chunk (noise-gate block), 1..8192 (capture.py:28, :64) */
@@ -316,7 +327,7 @@ void omega_ingest_config_default(omega_ingest_config* cfg);
 /* On an error after allocation *out is set: read omega_ingest_last_error, then omega_ingest_destroy. */
 int omega_ingest_create(omega_ctx* ctx, const omega_ingest_config* cfg, omega_ingest** out);
 int omega_ingest_push(omega_ingest* in, const void* bytes, int64_t n_bytes);
-/* Analyse the whole chunks buffered so far (the rest stays buffered). */
+/* Analyse the whole capture chunks buffered so far in whole frames (the rest stays buffered). */
 int omega_ingest_flush(omega_ingest* in);
 /* Up to max_frames completed frames (per channel) in frame order into host buffers laid out like
  * omega_outputs ([frames * C, T], [frames * C], [frames * C, 5]; NULL pointers skip); wait != 0

@@ -305,6 +305,31 @@ def gen_capture(R):
     np.savez_compressed(os.path.join(OUT, "capture.npz"), **d)
 
 
+def gen_capture_stereo(R):
+    """The same gate with an interleaved stereo capture (AudioCaptureConfig(channels=2)): the capture
+    loop reads chunk_size samples of the interleaved stream (capture.py:549-550) -- 256 frames of two
+    channels per chunk -- and _process_audio_frame gates each chunk as a whole. The left channel is
+    the mono golden's signal, the right one quieter (its own gaps keep the joint RMS up or let it fall).
+    Outputs, background level and silence counter after each chunk."""
+    d = {"versions": VERSIONS}
+    cap = R.PipeWireMonitorCapture("golden", R.AudioCaptureConfig(channels=2))
+    left = capture_signal()
+    n = len(left) // 2
+    rng = np.random.default_rng(23)
+    right = (0.3 * left[:n][::-1] + 0.0005 * rng.standard_normal(n)).astype(np.float32)
+    right[n // 3: n // 2] = 0.0
+    x = np.ascontiguousarray(np.stack([left[:n], right], axis=1))  # [n, 2] interleaved
+    flat = x.reshape(-1)
+    outs, bg, sil = [], [], []
+    for k in range(len(flat) // 512):
+        outs.append(np.array(cap._process_audio_frame(flat[k * 512:(k + 1) * 512])))
+        bg.append(float(cap.background_level))
+        sil.append(cap.silence_samples)
+    d["x"], d["out"] = x, np.concatenate(outs).astype(np.float32)
+    d["bg"], d["silence"] = np.array(bg), np.array(sil, np.int64)
+    np.savez_compressed(os.path.join(OUT, "capture_stereo.npz"), **d)
+
+
 def vu_frames(n=240, m=2048, seed=41):
     """The app's VU input: Hann-windowed float64 frames (omega4_main.py:1077-1082) of a tone whose level
     steps down (the display falls, the peak holds 2 s and then decays), then a silent stretch."""
@@ -588,6 +613,57 @@ class _Stop(Exception):
     pass
 
 
+def _post_app(R, M, A, kw):
+    """A stand-in analyzer object with the reference's own post-processing methods bound to it, the
+    real MultiResolutionFFT behind a recorder of each frame's combined spectrum and a drum detector
+    that stops process_audio_spectrum once spectrum and band values are final (:1069). run(x) feeds
+    one FFT_SIZE_BASE frame and returns (combined, spectrum, bands float64, content index)."""
+    app = SimpleNamespace()
+    for m in ("process_multi_resolution_fft", "update_content_type", "apply_frequency_compensation",
+              "auto_adjust_gain", "_create_equal_loudness_curve"):
+        setattr(app, m, types.MethodType(getattr(A, m), app))
+    mf = R.MultiResolutionFFT(FS)
+    rec = []
+
+    class Rec:
+        def process_audio_chunk(self, x, apply_weighting=True):
+            return mf.process_audio_chunk(x, apply_weighting)
+
+        def combine_results_optimized(self, res, target_bins=1024):
+            s, f = mf.combine_results_optimized(res, target_bins)
+            rec.append((s.copy(), f.copy()))
+            return s, f
+
+    class Drums:
+        def process_audio(self, spectrum, bands):
+            raise _Stop(spectrum.copy(), np.array(bands, dtype=np.float64))
+
+    prof = SimpleNamespace(profiler=SimpleNamespace(update_audio_latency=lambda *a: None))
+    bf = SimpleNamespace(prepare_batch=lambda *a, **k: 0, process_batch=lambda: 0, distribute_results=lambda: {})
+    app.__dict__.update(dict(
+        bars=512, freqs=np.fft.rfftfreq(M.FFT_SIZE_BASE, 1 / M.SAMPLE_RATE), multi_fft=Rec(),
+        psychoacoustic_enabled=True, freq_compensation_enabled=True, normalization_enabled=False,
+        smoothing_enabled=True, vocal_suppression=0.0, psycho_bass_boost=1.5, auto_gain_enabled=False,
+        voice_active=False, voice_confidence=0, adaptive_allocation_enabled=False,
+        current_content_type="instrumental", current_allocation=0.7, performance_profiler=prof,
+        batched_fft=bf, transient_events=[], last_transient_time=0.0, drum_detector=Drums(),
+        buffer_pos=M.FFT_SIZE_BASE, ring_buffer=np.zeros(M.FFT_SIZE_BASE * 4, np.float32)))
+    app.band_indices = R.PrecomputedFrequencyMapper(M.SAMPLE_RATE, M.FFT_SIZE_BASE, 512).mapping.band_indices
+    app.equal_loudness_curve = app._create_equal_loudness_curve()
+    app.__dict__.update(kw)
+
+    def run(x):
+        app.ring_buffer[:M.FFT_SIZE_BASE] = x
+        try:
+            A.process_audio_spectrum(app)
+            raise RuntimeError("process_audio_spectrum returned before drum detection")
+        except _Stop as e:
+            spec, bands = e.args
+        return (rec[-1][0], spec, bands, ("instrumental", "vocal", "bass_heavy").index(app.current_content_type))
+
+    return app, rec, run
+
+
 def gen_post(R):
     """The app's own per-frame post-processing, run through the reference's methods on a stand-in
     analyzer object: process_audio_spectrum (omega4_main.py:928-1056) calling the real
@@ -601,39 +677,7 @@ def gen_post(R):
     for name, kw in (("default", {}), ("vocal_supp_norm", {"vocal_suppression": 0.4, "normalization_enabled": True}),
                      ("flat", {"psychoacoustic_enabled": False, "freq_compensation_enabled": False,
                                "smoothing_enabled": False})):
-        app = SimpleNamespace()
-        for m in ("process_multi_resolution_fft", "update_content_type", "apply_frequency_compensation",
-                  "auto_adjust_gain", "_create_equal_loudness_curve"):
-            setattr(app, m, types.MethodType(getattr(A, m), app))
-        mf = R.MultiResolutionFFT(FS)
-        rec = []
-
-        class Rec:
-            def process_audio_chunk(self, x, apply_weighting=True):
-                return mf.process_audio_chunk(x, apply_weighting)
-
-            def combine_results_optimized(self, res, target_bins=1024):
-                s, f = mf.combine_results_optimized(res, target_bins)
-                rec.append((s.copy(), f.copy()))
-                return s, f
-
-        class Drums:
-            def process_audio(self, spectrum, bands):
-                raise _Stop(spectrum.copy(), np.array(bands, dtype=np.float64))
-
-        prof = SimpleNamespace(profiler=SimpleNamespace(update_audio_latency=lambda *a: None))
-        bf = SimpleNamespace(prepare_batch=lambda *a, **k: 0, process_batch=lambda: 0, distribute_results=lambda: {})
-        app.__dict__.update(dict(
-            bars=512, freqs=np.fft.rfftfreq(M.FFT_SIZE_BASE, 1 / M.SAMPLE_RATE), multi_fft=Rec(),
-            psychoacoustic_enabled=True, freq_compensation_enabled=True, normalization_enabled=False,
-            smoothing_enabled=True, vocal_suppression=0.0, psycho_bass_boost=1.5, auto_gain_enabled=False,
-            voice_active=False, voice_confidence=0, adaptive_allocation_enabled=False,
-            current_content_type="instrumental", current_allocation=0.7, performance_profiler=prof,
-            batched_fft=bf, transient_events=[], last_transient_time=0.0, drum_detector=Drums(),
-            buffer_pos=M.FFT_SIZE_BASE, ring_buffer=np.zeros(M.FFT_SIZE_BASE * 4, np.float32)))
-        app.band_indices = R.PrecomputedFrequencyMapper(M.SAMPLE_RATE, M.FFT_SIZE_BASE, 512).mapping.band_indices
-        app.equal_loudness_curve = app._create_equal_loudness_curve()
-        app.__dict__.update(kw)
+        app, rec, run = _post_app(R, M, A, kw)
         t = np.arange(M.FFT_SIZE_BASE) / FS
         comb, spec, bands, content = [], [], [], []
         for i in range(24):
@@ -641,15 +685,8 @@ def gen_post(R):
             f0 = (55.0, 700.0, 2500.0)[i % 3] * (1 + 0.05 * i)
             x = (0.4 * np.sin(2 * np.pi * f0 * t) + 0.2 * np.sin(2 * np.pi * 3.1 * f0 * t)
                  + 0.02 * (i % 4) * rng.standard_normal(len(t))).astype(np.float32)
-            app.ring_buffer[:M.FFT_SIZE_BASE] = x
-            try:
-                A.process_audio_spectrum(app)
-                raise RuntimeError("process_audio_spectrum returned before drum detection")
-            except _Stop as e:
-                spec.append(e.args[0])
-                bands.append(e.args[1])
-            comb.append(rec[-1][0])
-            content.append(("instrumental", "vocal", "bass_heavy").index(app.current_content_type))
+            c, s_, b, k = run(x)
+            comb.append(c), spec.append(s_), bands.append(b), content.append(k)
         d[f"{name}/combined"] = np.stack(comb).astype(np.float32)
         d[f"{name}/freqs"] = rec[-1][1]
         d[f"{name}/spectrum"] = np.stack(spec)
@@ -658,11 +695,69 @@ def gen_post(R):
     np.savez_compressed(os.path.join(OUT, "app_post.npz"), **d)
 
 
+def gen_post_ema(R):
+    """The band EMA through a silence (omega4_main.py:1041-1056), from the reference's own loop: 1000
+    frames of a note whose pitch and level drift, every fifth frame broadband noise (the note frames'
+    bands clamp to the int 1, so their band arrays are float64; the noise frames' are float32), then 500 silent frames over which every band decays
+    towards the smallest float32 denormal. Stores the combined spectra up to the last non-zero one (the
+    later ones are zero), the band values of every frame and the content types."""
+    M = _import_app()
+    A = M.ProfessionalLiveAudioAnalyzer
+    app, rec, run = _post_app(R, M, A, {})
+    t = np.arange(M.FFT_SIZE_BASE) / FS
+    rng = np.random.default_rng(21)
+    comb, bands, content, f64 = [], [], [], []
+    n_note, n_sil = 1000, 500
+    for i in range(n_note + n_sil):
+        if i < n_note and i % 5 == 4:  # broadband frames: no band clamps, a float32 band array
+            x = (0.2 * rng.standard_normal(M.FFT_SIZE_BASE)).astype(np.float32)
+        elif i < n_note:
+            f0 = 330.0 * (1 + 0.25 * np.sin(i / 37.0))
+            a = 0.3 * (1 + 0.8 * np.sin(i / 11.0) ** 2)
+            x = (a * np.sin(2 * np.pi * f0 * t) + 0.3 * a * np.sin(2 * np.pi * 2.02 * f0 * t)).astype(np.float32)
+        else:
+            x = np.zeros(M.FFT_SIZE_BASE, np.float32)
+        c, _, b, k = run(x)
+        comb.append(c)
+        bands.append(b)
+        content.append(k)
+        f64.append(app.prev_band_values.dtype == np.float64)
+    # the resolutions' ring buffers still hold note samples for a few silent frames: keep the combined
+    # spectra up to the last non-zero one (the rest are zero)
+    comb = np.stack(comb).astype(np.float32)
+    nz = int(np.flatnonzero(comb.any(axis=1))[-1]) + 1
+    np.savez_compressed(os.path.join(OUT, "post_ema.npz"), versions=VERSIONS, freqs=rec[-1][1],
+                        combined=comb[:nz], n_frames=np.int64(n_note + n_sil), n_silent=np.int64(n_sil),
+                        bands=np.stack(bands), content=np.array(content, np.int32),
+                        band_f64=np.array(f64, bool))
+
+
+def gen_post_threshold(R):
+    """Content-type labels of tests/golden/post_threshold.npz's frames (combined spectra whose bass
+    ratio sits within a few float32 ulps of 0.6; tests/golden/gen_post_threshold.py chose them) from the
+    reference's own update_content_type (omega4_main.py:805-840) on the app's float32 spectrum, with
+    the psychoacoustic curve off as in the test -- the labels are the reference's, not the oracle's."""
+    M = _import_app()
+    A = M.ProfessionalLiveAudioAnalyzer
+    path = os.path.join(OUT, "post_threshold.npz")
+    g = dict(np.load(path))
+    app = SimpleNamespace(voice_active=False, voice_confidence=0, adaptive_allocation_enabled=False,
+                          current_content_type="instrumental")
+    labels = []
+    for s in g["combined"]:
+        A.update_content_type(app, np.array(s, np.float32), None)
+        labels.append(("instrumental", "vocal", "bass_heavy").index(app.current_content_type))
+    g["content"] = np.array(labels, np.int32)
+    g["versions"] = VERSIONS
+    g["labels_source"] = np.array("reference omega4_main.ProfessionalLiveAudioAnalyzer.update_content_type")
+    np.savez_compressed(path, **g)
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac", "meters_any", "mrfft_small", "transients_any"))]:
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac", "meters_any", "mrfft_small", "transients_any", "post_ema", "post_threshold", "capture_stereo"))]:
         g(R)
         print("wrote", g.__name__)

@@ -913,6 +913,23 @@ def capture_stream(x: np.ndarray, fs: int = 48000, chunk: int = 512, gain: float
     return y * gain
 
 
+def capture_stream_interleaved(x: np.ndarray, fs: int = 48000, chunk: int = 512, gain: float = 4.0,
+                               gate: bool = True) -> np.ndarray:
+    """The analysed streams of an interleaved capture x [n, C]: the capture loop reads chunk_size
+    samples of the interleaved stream whatever the channel count (capture.py:549-550), so one gate
+    (one RMS over all the chunk's channels, one state) runs over the flattened stream; then the
+    input gain. Returns planar [C, n'] over the whole chunks, cut to whole frames."""
+    x = np.asarray(x)
+    C = x.shape[1]
+    flat = x.reshape(-1)
+    n = len(flat) // chunk * chunk
+    g = CaptureGate(fs, chunk)
+    y = np.concatenate([g.process(flat[i:i + chunk]) if gate else flat[i:i + chunk] for i in range(0, n, chunk)]) \
+        if n else np.zeros(0, np.float32)
+    y = y[:len(y) // C * C]
+    return (y * gain).reshape(-1, C).T.copy()
+
+
 def s16le_samples(data: bytes) -> np.ndarray:
     """capture.py:571-574 for s16le: int16 -> float32 / 32768.0."""
     return np.frombuffer(data, dtype=np.int16).astype(np.float32) / 32768.0

@@ -105,3 +105,21 @@ def test_product_package_does_not_import_oracle():
         if f.endswith(".py"):
             src = open(os.path.join(pkg, f)).read()
             assert not re.search(r"^\s*(from|import)\s+(oracle|scipy)\b", src, flags=re.M), f
+
+
+def test_abi_guard_maps_host_allocation_failure(tmp_path):
+    """include/omega.h's contract -- no C++ exception crosses the ABI -- through public entry points:
+    tests/abi/abi_guard.cpp replaces operator new with one that throws std::bad_alloc while armed and
+    calls omega_create and omega_post_configure (a host-side table build) armed; both return
+    OMEGA_ENOMEM with a message instead of terminating the process (no GPU needed)."""
+    import shutil
+    import subprocess
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    lib = os.path.join(REPO, "audio-analyzer-omega_amd", "lib")
+    exe = str(tmp_path / "abi_guard")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-o", exe, os.path.join(REPO, "tests", "abi", "abi_guard.cpp"),
+                    f"-L{lib}", "-lomega", f"-Wl,-rpath,{lib}"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().endswith("ok")

@@ -140,10 +140,14 @@ def test_k_weighting_golden(me, name):
 
 
 def test_k_weighting_coefficients(me):
+    """k_weighting_filter and create_k_weighting_filter (professional_meters.py:48-72) against the
+    reference's scipy coefficients (golden), the unused shelf gain included."""
     from omega_gpu.professional_meters import ProfessionalMetering
-    kf = ProfessionalMetering(FS).k_weighting_filter
-    for k, g in (("hp_b", "coef/hp_b"), ("hp_a", "coef/hp_a"), ("shelf_b", "coef/sh_b"), ("shelf_a", "coef/sh_a")):
-        np.testing.assert_allclose(kf[k], me[g], rtol=1e-12, atol=1e-15)
+    pm = ProfessionalMetering(FS)
+    for kf in (pm.k_weighting_filter, pm.create_k_weighting_filter()):
+        for k, g in (("hp_b", "coef/hp_b"), ("hp_a", "coef/hp_a"), ("shelf_b", "coef/sh_b"), ("shelf_a", "coef/sh_a")):
+            np.testing.assert_allclose(kf[k], me[g], rtol=1e-12, atol=1e-15)
+        assert kf["shelf_gain"] == 10 ** (4.0 / 20)
 
 
 @pytest.mark.parametrize("name", ["cfg2L", "sine2048", "low50_4096", "silence", "steps1024", "square1024"])
@@ -278,18 +282,20 @@ def test_meters_any_length_golden(name):
     assert normwise(y, g[f"{name}/kw0"]) < 1e-6
 
 
-@pytest.mark.parametrize("m", [1024, 8192, 16384])
+@pytest.mark.parametrize("m", [1, 2, 3, 100, 1000, 1024, 8192, 16384])
 def test_true_peak_oversampling(m):
     """calculate_true_peak(x, oversampling) for 1, 2 and 4 (phase subsets of the polyphase transform)
-    against scipy's resample (the oracle); an unsupported factor is logged and the previous value
-    returned."""
+    against scipy's resample (the oracle), at every frame length omega_true_peak_os accepts (m >= 1:
+    the power-of-two kernels and the mixed-radix path down to one sample); an unsupported factor is
+    logged and the previous value returned."""
     from omega_gpu.professional_meters import ProfessionalMetering
     pm = ProfessionalMetering(FS)
     x = S.sine(997, 0.4, m) + S.noise(31, m, 0.05)
     for o in (4, 2, 1):
         got = pm.calculate_true_peak(x, o)
         assert abs(got - R.true_peak(x, o)) < TP_TOL_DB, (m, o)
-    assert pm.calculate_true_peak(x, 4) > pm.calculate_true_peak(x, 2) - 1e-6 > pm.calculate_true_peak(x, 1) - 2e-6
+    tp4, tp2, tp1 = (float(pm.calculate_true_peak(x, o)) for o in (4, 2, 1))
+    assert tp4 >= tp2 - 1e-4 and tp2 >= tp1 - 1e-4  # more phases never lower the peak
     prev = pm.calculate_true_peak(x, 4)
     assert pm.calculate_true_peak(x, 3) == prev
 
@@ -736,6 +742,65 @@ def test_spectra_cfg3_vs_oracle():
     np.testing.assert_array_equal(out["bands"], bt.apply(out["mag"]))
 
 
+def test_spectra_cfg3_full_batch():
+    """The launch bench.py's cfg3 line times: 4096 frames x 8192 in one omega_spectra call (bands with
+    the compensation scale + chromagram, device input, no magnitudes). Every output finite, bands and
+    chroma non-negative, chroma normalised (sum 1 on every frame with energy); sampled frames across
+    the batch (first, last, both parities, XCD/round boundaries) against the oracle chain."""
+    import torch
+    from omega_gpu import Engine, Resolution
+    from omega_gpu.engine import BandTable
+    from omega_gpu import _lib as L
+    n = 4096
+    x = S.cfg3_batch(n)
+    eng = Engine([Resolution((20, 20000), 8192, 2048, 1.0)], FS, 20000, 512)
+    st, en, comp = R.pipeline_band_table(FS, 512, 8192)
+    bt = BandTable(eng, L.BANDS_MAX, st, en, 512, 4097, scale=comp)
+    xd = torch.from_numpy(x).cuda()
+    out = eng.spectra(xd, "hann", bands=bt, chroma=True)
+    torch.cuda.synchronize()
+    bands, chroma = out["bands"].cpu().numpy(), out["chroma"].cpu().numpy()
+    assert bands.shape == (n, 512) and chroma.shape == (n, 12)
+    assert np.isfinite(bands).all() and np.isfinite(chroma).all()
+    assert (bands >= 0).all() and (chroma >= 0).all()
+    np.testing.assert_allclose(chroma.sum(axis=1), 1.0, rtol=1e-12)
+    freqs = np.fft.rfftfreq(8192, 1 / FS)
+    rng = np.random.default_rng(3)
+    sample = sorted({0, 1, 7, 8, 255, 256, 1023, 1024, 2047, 2048, 4094, 4095} | set(rng.integers(0, n, 8).tolist()))
+    for f in sample:
+        mag = R.batched_fft(x[f], 8192, "hann")["magnitude"]
+        want = R.map_to_bands(mag.astype(np.float32), st, en, comp, 512)
+        np.testing.assert_allclose(bands[f], want, rtol=1e-4, atol=1e-6 * np.max(want), err_msg=f"frame {f}")
+        ch = R.ChromaState().compute(mag.astype(np.float32), freqs)
+        np.testing.assert_allclose(chroma[f], ch, rtol=1e-5, atol=1e-9, err_msg=f"frame {f}")
+
+
+def test_cfg1_stream_momentary_lufs():
+    """BASELINE cfg1 (configs[0]): one 48 kHz mono stream, hop 512, W = 1024, one 1024-point
+    resolution, 600 frames of 0.5 sin(2 pi 1000 t): the combined spectrum, LUFS_inst and the meter
+    aggregates (momentary over the last 24 frames) of every frame against the oracle's per-frame loop
+    (calculate_lufs fed frame by frame)."""
+    from omega_gpu import Engine, Resolution
+    W, H, F = 1024, 512, 600
+    n = W + H * (F - 1)
+    x = S.sine(1000, 0.5, n)
+    eng = Engine([Resolution((20, 20000), W, H, 1.0)], FS, 20000, target_bins=512, frame_size=W)
+    out = eng.process_stream(x, n, H, combined=True, meters=True)
+    assert out["lufs_inst"].shape == (F,)
+    st = R.MeterState(FS)
+    cfgs = (R.FFTConfig((20, 20000), W, H, 1.0),)
+    for f in range(F):
+        fr = x[f * H:f * H + W]
+        _, comb, li, tp = R.full_frame(fr, configs=cfgs, target_bins=512)
+        assert normwise(out["combined"][f], comb) < SPEC_TOL, f
+        assert abs(out["lufs_inst"][f] - li) < LU_TOL, f
+        assert abs(out["true_peak_db"][f] - tp) < TP_TOL_DB, f
+        agg = st.update(fr, li, tp)
+        assert abs(out["meters"][f][0] - agg["momentary"]) < LU_TOL, f
+        assert abs(out["meters"][f][1] - agg["short_term"]) < LU_TOL, f
+        assert abs(out["meters"][f][4] - agg["true_peak"]) < TP_TOL_DB, f
+
+
 def test_cfg5_stream_96k_surround():
     """BASELINE cfg5 shape at small size: 96 kHz, 8 channels, stream layout (hop 1024) of 16384-point
     frames with true peak, K-weighted LUFS (filters designed for 96 kHz) and the meter aggregates,
@@ -827,22 +892,68 @@ POST_CFG = {"default": ({}, {}),
                                 dict(vocal_suppression=0.4, normalization_enabled=True)),
             "flat": (dict(psycho=False, freq_comp=False, smoothing=False),
                      dict(psychoacoustic_enabled=False, freq_compensation_enabled=False, smoothing_enabled=False))}
-# band means: float64 sums on the device vs numpy's float32 pairwise sums, then sqrt and the EMA
-POST_BAND_RTOL, POST_BAND_ATOL = 2e-6, 1e-7
-
-
 @pytest.mark.parametrize("name", sorted(POST_CFG))
 def test_app_post_golden(name):
-    """The app's own post-processing (golden, gen_golden.gen_post) from its combined spectra: the
-    spectrum bit-exact (the same float32 operations), content types equal, band values to float32
-    rounding."""
+    """The app's own post-processing (golden, gen_golden.gen_post) from its combined spectra: spectrum,
+    content types and band values bit-exact."""
     from omega_gpu.app_post import SpectrumPostProcessor
     g = load_golden("app_post")
     pp = SpectrumPostProcessor(g[f"{name}/freqs"], **POST_CFG[name][1])
     s, b, c = pp.process(g[f"{name}/combined"])
     np.testing.assert_array_equal(s, g[f"{name}/spectrum"])
     np.testing.assert_array_equal(c, g[f"{name}/content"])
-    np.testing.assert_allclose(b, g[f"{name}/bands"], rtol=POST_BAND_RTOL, atol=POST_BAND_ATOL)
+    np.testing.assert_array_equal(b, g[f"{name}/bands"])
+
+
+def _post_ema_input(g):
+    c = np.zeros((int(g["n_frames"]), g["combined"].shape[1]), np.float32)
+    c[:len(g["combined"])] = g["combined"]
+    return c
+
+
+def test_app_post_ema_through_silence_golden():
+    """The reference's own loop over 1000 note frames and 500 silent ones (gen_golden.gen_post_ema):
+    band values bit-exact through the silence -- the bands keep decaying into float32 denormals where a
+    chunk warmed up from silent frames alone would sit at 0 -- in one 1500-frame call (24 EMA chunks)
+    and in calls of 1, 63, 700 and the rest."""
+    from omega_gpu.app_post import SpectrumPostProcessor
+    g = load_golden("post_ema")
+    x = _post_ema_input(g)
+    pp = SpectrumPostProcessor(g["freqs"])
+    s, b, c = pp.process(x)
+    np.testing.assert_array_equal(b, g["bands"])
+    np.testing.assert_array_equal(c, g["content"])
+    assert (b[-1] < 1e-30).all() and (b[-1] > 0).sum() > 400
+    pp.reset()
+    parts = [pp.process(x[a:e])[1] for a, e in ((0, 1), (1, 64), (64, 764), (764, len(x)))]
+    np.testing.assert_array_equal(np.concatenate(parts), g["bands"])
+
+
+def test_app_post_ema_slow_factors_exact():
+    """EMA factors up to 0.995 (the warm-up no longer fades out within a chunk's 256-frame lead: the
+    fix pass re-runs those chunks) give the sequential recurrence bit for bit in one 900-frame call."""
+    import omega_gpu.app_post as AP
+    g = load_golden("app_post")
+    freqs = g["default/freqs"]
+    rng = np.random.default_rng(17)
+    x = (rng.random((900, 512)) * rng.random((900, 1)) ** 2).astype(np.float32)
+    x[300:700] = 0.0
+    orig_dev, orig_ref = AP._band_table, R.app_band_table
+
+    def slow_dev(*a):
+        bs, be, f = orig_dev(*a)
+        return bs, be, np.linspace(0.9, 0.995, len(f))
+
+    def slow_ref(*a):
+        keep, f = orig_ref(*a)
+        return keep, list(np.linspace(0.9, 0.995, len(f)))
+    try:
+        AP._band_table, R.app_band_table = slow_dev, slow_ref
+        _, b, _ = AP.SpectrumPostProcessor(freqs).process(x)
+        _, wb, _ = R.app_post_sequence(x, freqs)
+    finally:
+        AP._band_table, R.app_band_table = orig_dev, orig_ref
+    np.testing.assert_array_equal(b, wb)
 
 
 def test_app_post_content_threshold_frames():
@@ -850,7 +961,7 @@ def test_app_post_content_threshold_frames():
     and numpy's float32 pairwise np.mean disagree (tests/golden/gen_post_threshold.py): the device
     classifies as the reference does."""
     from omega_gpu.app_post import SpectrumPostProcessor
-    g = np.load(os.path.join(GOLDEN, "post_threshold.npz"))
+    g = np.load(os.path.join(GOLDEN, "post_threshold.npz"))  # labels: the reference's update_content_type
     assert (g["content"] != g["content_f64"]).all()
     freqs = load_golden("app_post")["default/freqs"]
     pp = SpectrumPostProcessor(freqs, psychoacoustic_enabled=False, freq_compensation_enabled=False)
@@ -922,7 +1033,7 @@ def test_app_post_random_state_and_device_input():
     s, b, c = pp.process(x)
     np.testing.assert_array_equal(s, ws)
     np.testing.assert_array_equal(c, wc)
-    np.testing.assert_allclose(b, wb, rtol=POST_BAND_RTOL, atol=POST_BAND_ATOL)
+    np.testing.assert_array_equal(b, wb)
     pp.reset()
     xd = torch.zeros((F, 640), dtype=torch.float32, device="cuda")
     xd[:, :512] = torch.from_numpy(x).cuda()
@@ -934,9 +1045,9 @@ def test_app_post_random_state_and_device_input():
 
 
 def test_app_post_ema_chunks_join_the_sequential_recurrence():
-    """700 frames in one call (the band EMA runs as 6 chunks of 128 frames, the later ones warmed up
-    over the 256 frames before them) give bit for bit the bands of 7 sequential calls of 100 frames
-    (each one chunk that continues the carried state), and match the oracle."""
+    """700 frames in one call (the band EMA runs as 11 chunks of 64 frames, the later ones warmed up
+    over the 256 frames before them and checked against the sequential state) give bit for bit the
+    bands of 7 sequential calls of 100 frames, and the oracle's."""
     from omega_gpu.app_post import SpectrumPostProcessor
     freqs = load_golden("app_post")["default/freqs"]
     rng = np.random.default_rng(12)
@@ -947,4 +1058,4 @@ def test_app_post_ema_chunks_join_the_sequential_recurrence():
     np.testing.assert_array_equal(b1, np.concatenate([p[1] for p in parts]))
     np.testing.assert_array_equal(s1, np.concatenate([p[0] for p in parts]))
     ws, wb, wc = R.app_post_sequence(x, freqs)
-    np.testing.assert_allclose(b1, wb, rtol=POST_BAND_RTOL, atol=POST_BAND_ATOL)
+    np.testing.assert_array_equal(b1, wb)

@@ -77,8 +77,36 @@ def test_ingest_golden_capture_gate_mono():
     assert silent and all(out["lufs_inst"][f] == -100.0 for f in silent)
 
 
+def test_ingest_golden_capture_gate_stereo():
+    """The reference-recorded interleaved stereo capture (gen_golden.gen_capture_stereo: the gate reads
+    512 interleaved samples at a time, one RMS and one state for both channels) pushed as float32le
+    bytes in irregular pieces: the gated stream is the golden one (silent frames exactly where the
+    joint gate closed), every frame of both channels against the oracle."""
+    from omega_gpu import Engine, Resolution
+    from omega_gpu.ingest import StreamIngest
+    g = load_golden("capture_stereo")
+    x = g["x"]
+    W, H = 2048, 512
+    eng = Engine([Resolution((20, 20000), W, H, 1.0)], 48000, 20000, target_bins=128, frame_size=W, n_channels=2)
+    ing = StreamIngest(eng, hop=H, batch_hops=16, ring_slots=3, gain=4.0)
+    got = []
+    for p in _pieces(x.tobytes()):
+        ing.push(p)
+        got.append(ing.poll())
+    ing.flush()
+    got.append(ing.poll(wait=True))
+    out = {k: np.concatenate([d[k] for d in got]) for k in got[0]}
+    y = R.capture_stream_interleaved(x, gain=4.0)
+    np.testing.assert_array_equal(y.T.reshape(-1), g["out"][:y.size] * np.float32(4.0))
+    F = (y.shape[1] - W) // H + 1
+    assert len(out["lufs_inst"]) == 2 * F and ing.stats()["dropped_frames"] == 0
+    _check_frames(out, [y[0], y[1]], 48000, W, H, set(range(0, F, 3)) | {F - 1}, 2)
+    silent = [f for f in range(F) if not y[:, f * H:f * H + W].any()]
+    assert silent and all(out["lufs_inst"][2 * f + c] == -100.0 for f in silent for c in range(2))
+
+
 def test_ingest_s16le_stereo_and_drop_policy():
-    """Interleaved s16le stereo (int16 / 32768, per-channel gate), never polled while 8 batches go
+    """Interleaved s16le stereo (int16 / 32768, one gate over the interleaved chunks), never polled while 8 batches go
     through with room for 3 pending result blocks: the oldest results are dropped and counted, the
     last ones still match the oracle."""
     from omega_gpu import Engine, Resolution
@@ -98,7 +126,7 @@ def test_ingest_s16le_stereo_and_drop_policy():
     assert st["batches"] == 8 and st["dropped_frames"] > 0
     out = ing.poll(wait=True)
     dropped = ing.stats()["dropped_frames"]
-    streams = [R.capture_stream(R.s16le_samples(pcm[c].tobytes()), gain=2.0) for c in range(2)]
+    streams = R.capture_stream_interleaved(R.s16le_samples(inter.tobytes()).reshape(-1, 2), gain=2.0)
     F = (n - W) // H + 1
     assert dropped + len(out["lufs_inst"]) // 2 == F
     # the surviving frames are the last ones of the stream
@@ -136,7 +164,7 @@ def test_ingest_cfg5_past_integrated_window():
     got.append(ing.poll(wait=True))
     out = {k: np.concatenate([d[k] for d in got]) for k in got[0]}
     assert len(out["lufs_inst"]) == F * C and ing.stats()["dropped_frames"] == 0
-    streams = [R.capture_stream(x[c], fs=fs, gain=1.0) for c in range(C)]
+    streams = R.capture_stream_interleaved(inter, fs=fs, gain=1.0)
     assert all(np.array_equal(streams[c], x[c][:len(streams[c])]) for c in range(C))  # the gate stays open
     sample = {0, 1, 63, 64, 2047, 3599, 3600, F - 1}
     for c in (0, 7):

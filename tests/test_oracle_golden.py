@@ -308,6 +308,46 @@ def test_app_post(name):
     assert set(c.tolist()) >= {1, 2}
 
 
+def test_capture_gate_stereo_interleaved():
+    """The reference's gate on an interleaved stereo capture (gen_golden.gen_capture_stereo: chunks of
+    512 interleaved samples, one RMS and one state for both channels): the restatement's
+    capture_stream_interleaved gives the golden chunks bit for bit, and differs from gating each
+    channel on its own."""
+    g = load_golden("capture_stereo")
+    y = R.capture_stream_interleaved(g["x"], gain=1.0)
+    np.testing.assert_array_equal(y.T.reshape(-1), g["out"][:y.size])
+    per_channel = np.stack([R.capture_stream(g["x"][:, c], gain=1.0) for c in range(2)])
+    assert not np.array_equal(per_channel[:, :y.shape[1]], y)
+
+
+def post_ema_input(g):
+    """post_ema.npz's combined spectra, padded with the zero spectra of the silent tail."""
+    c = np.zeros((int(g["n_frames"]), g["combined"].shape[1]), np.float32)
+    c[:len(g["combined"])] = g["combined"]
+    return c
+
+
+def test_app_post_ema_through_silence():
+    """The reference's own loop (gen_golden.gen_post_ema) over 1000 note frames and 500 silent ones:
+    the restatement's band EMA is bit-exact, float64 band arrays on the clamping frames and the decay
+    into float32 denormals included."""
+    g = load_golden("post_ema")
+    s, b, c = R.app_post_sequence(post_ema_input(g), g["freqs"])
+    np.testing.assert_array_equal(b, g["bands"])
+    np.testing.assert_array_equal(c, g["content"])
+    tail = b[-1]
+    assert g["band_f64"][:1000].any() and not g["band_f64"][-100:].any()
+    assert (tail < 1e-30).all() and (tail > 0).sum() > 400  # still decaying, not 0
+
+
+def test_app_post_threshold_labels_are_the_references():
+    """post_threshold.npz's labels come from the reference's update_content_type
+    (gen_golden.gen_post_threshold), and the restatement agrees with them."""
+    g = load_golden("post_threshold")
+    assert "reference" in str(g["labels_source"])
+    np.testing.assert_array_equal([R.app_content_type(x) for x in g["combined"]], g["content"])
+
+
 def test_capture_gate(golden):
     """The capture noise gate (golden: the reference's own _process_audio_frame, chunk by chunk): the
     gated chunks, the background level (float32 after its first update) and the silence counter."""

@@ -20,13 +20,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("stage")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--frames", type=int, default=256, help="stereo frames per call (cfg2: 256, cfg4 shard: 4096)")
     a = ap.parse_args()
     import bench
     from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
     from omega_gpu import _lib as L
-    x = torch.from_numpy(bench.cfg2_input()).cuda()
+    F = a.frames
+    x = torch.from_numpy(bench.cfg2_input(F)).cuda()
     eng = Engine(NORTHSTAR_RESOLUTIONS, 48000, 20000, target_bins=512, n_channels=2)
-    ncf = 512
+    ncf = 2 * F
     lib = L.lib()
     eng._bind_stream(x)
     out = {k: torch.empty(ncf, device="cuda") for k in ("tp", "li")}
@@ -51,7 +53,7 @@ def main():
     def run():
         if a.stage == "batch":  # one batch_kernel launch: the step's per-channel-frame work, no meters
             import ctypes
-            eng._check(lib.omega_process_frames(eng._ctx, x.data_ptr(), 256, 2 * 16384, 16384, ctypes.byref(outs),
+            eng._check(lib.omega_process_frames(eng._ctx, x.data_ptr(), F, 2 * 16384, 16384, ctypes.byref(outs),
                                                 L.MEM_DEVICE))
         if a.stage == "spectra":
             e3.spectra(x3, "hann", bands=bt, chroma=True, out=so)
@@ -62,10 +64,10 @@ def main():
         if a.stage in ("kw", "all"):
             eng._check(lib.omega_k_weighting(eng._ctx, x.data_ptr(), ncf, 16384, None, out["li"].data_ptr(), L.MEM_DEVICE))
         if a.stage in ("mrfft", "all"):
-            eng.process_frames(x, 256, 2 * 16384, 16384, combined=True, lufs=False, true_peak=False,
+            eng.process_frames(x, F, 2 * 16384, 16384, combined=True, lufs=False, true_peak=False,
                                out={"combined": comb})
         if a.stage in ("meters", "all"):
-            eng._check(lib.omega_meter_update(eng._ctx, out["li"].data_ptr(), out["tp"].data_ptr(), 256,
+            eng._check(lib.omega_meter_update(eng._ctx, out["li"].data_ptr(), out["tp"].data_ptr(), F,
                                               met.data_ptr(), L.MEM_DEVICE))
     for _ in range(3):
         run()
@@ -77,8 +79,8 @@ def main():
     e.record()
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / a.reps * 1e3
-    print(f"{a.stage}: {us:.1f} us per call" + (f" = {ncf / us * 1e6:.0f} channel-frames/s (host in/out)"
-                                                  if a.stage == "host" else ""))
+    print(f"{a.stage}: {us:.1f} us per call, {us * 1e3 / ncf:.1f} ns per channel-frame ({ncf} cf)" +
+          (f" = {ncf / us * 1e6:.0f} channel-frames/s (host in/out)" if a.stage == "host" else ""))
 
 
 if __name__ == "__main__":
