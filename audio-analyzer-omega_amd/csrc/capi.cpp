@@ -30,6 +30,8 @@ hipError_t launch_mrfft_range(const SpectralParams& p, int r0, int r1, hipStream
 hipError_t launch_mrfft_independent(const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s);
+hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s);
+hipError_t launch_mrfft_rf_pair(const SpectralParams& p, int r, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
 hipError_t launch_weight64(const Weight64Params& p, hipStream_t s);
@@ -1172,6 +1174,37 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
 extern "C" {
 
 const char* omega_version(void) { return "omega-mi355x 0.1 (gfx950, ABI 1)"; }
+
+#ifdef OMEGA_STAMPS
+// Development build only (make dev): one kernel variant over n_cf channel-frames of the context's
+// frames x (device memory, frame stride W, channel stride W * ... as omega_process_frames with
+// frame_stride = C * W, channel_stride = W), outputs to device buffers. which: 0 the 16384-point
+// resolution single-frame kernel, 1 its two-frames-per-workgroup form (combine of resolution 0);
+// 2 the true-peak kernel (aux: [n_cf] true peaks). (A two-frames-per-workgroup true peak, its spectrum
+// parked in L2 scratch between phases, measured no faster at 8192 channel-frames: 614 vs 621 us, the
+// shader clock 1773 vs 1897 MHz -- the extra frames in flight bought activity, and the clock gave it
+// back.)
+int omega_dev_probe(omega_ctx* c, int which, const float* x, int64_t n_frames, float* comb, float* aux) {
+  SpectralParams sp = spectral_params(c);
+  const int W = c->cfg.frame_size;
+  sp.x = x;
+  sp.frame_stride = (int64_t)c->cfg.n_channels * W;
+  sp.chan_stride = W;
+  sp.n_cf = n_frames * c->cfg.n_channels;
+  sp.comb_out = comb;
+  (void)aux;
+  for (int r = 0; r < kMaxRes; ++r) sp.res[r].mag_out = nullptr;
+  hipError_t e = hipErrorInvalidValue;
+  sp.tp_out = aux;
+  float2* rot = nullptr;
+  if (int r = get_rot(c, W, &rot)) return r;
+  sp.rot = rot;
+  if (which == 0) e = launch_mrfft_rf(16384, sp, 0, c->stream);
+  if (which == 1) e = launch_mrfft_rf_pair(sp, 0, c->stream);
+  if (which == 2) e = launch_truepeak_rf(16384, sp, c->stream);
+  return e == hipSuccess ? 0 : fail(c, OMEGA_EHIP, "probe %d: %s", which, hipGetErrorString(e));
+}
+#endif
 
 void omega_config_default(omega_config* cfg) try {
   std::memset(cfg, 0, sizeof *cfg);

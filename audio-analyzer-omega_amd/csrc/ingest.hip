@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void ingest_rms_kernel(IngestParams p) {
     sq[i] = v * v;
   }
   __syncthreads();
-  if (threadIdx.x == 0) p.rms[k] = __fsqrt_rn(np_mean_f32(sq, p.chunk));
+  if (threadIdx.x == 0) p.rms[k] = np_sqrt_f32(np_mean_f32(sq, p.chunk));
 }
 
 // the gate state machine of _process_audio_frame, chunk by chunk (one thread: the stream's state)

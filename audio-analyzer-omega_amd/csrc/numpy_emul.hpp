@@ -6,6 +6,24 @@
 
 namespace omega {
 
+// np.sqrt of a float32: the correctly rounded square root. The hardware square root (v_sqrt_f32,
+// what __fsqrt_rn lowers to here) is within 1 ulp, not correctly rounded (measured: 0.41999188 ->
+// 0.64806777, numpy 0.64806783); one correction step against the neighbours' rounding midpoints, in
+// float64 where the squares are exact, gives numpy's value. Non-positive, infinite and NaN inputs
+// pass through the hardware result (exact there).
+__device__ __forceinline__ float np_sqrt_f32(float x) {
+  float r = __builtin_sqrtf(x);
+  if (!(x > 0.f) || !(x < INFINITY)) return r;
+  const double xd = x;
+  const float up = __uint_as_float(__float_as_uint(r) + 1u);
+  const double mu = 0.5 * ((double)r + (double)up);  // exact: 25 significant bits
+  if (xd >= mu * mu) return up;                      // (a tie cannot occur: x has 24 bits, mu^2 more)
+  const float dn = __uint_as_float(__float_as_uint(r) - 1u);
+  const double md = 0.5 * ((double)r + (double)dn);
+  if (xd < md * md) return dn;
+  return r;
+}
+
 // numpy's pairwise_sum for contiguous float32 (numpy/_core/src/umath/loops_utils.h.src): below 8
 // elements a plain running sum, up to 128 eight interleaved accumulators combined as
 // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) plus the tail, above that the two halves split at a

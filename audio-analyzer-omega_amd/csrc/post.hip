@@ -243,7 +243,7 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
       v = s[lo];
     }
     if (v > 0.f) {
-      v = __fsqrt_rn(v);
+      v = np_sqrt_f32(v);
       if (!(v < 1.0f)) {
         v = 1.0f;
         clamp_any = 1;

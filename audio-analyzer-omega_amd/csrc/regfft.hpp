@@ -213,6 +213,87 @@ struct RegFFT {
     }
   }
 
+  // The pass bodies of run2() as separate steps, for run_pair().
+  static __device__ __forceinline__ void pass1(float2 (&v)[16], float2 w1) {
+    dft16(v);
+    twiddle(v, w1);
+  }
+  static __device__ __forceinline__ void write1(const float2 (&v)[16], float2* buf, int t1) {
+    float2* b = buf + t1;
+    static_for<0, 16>([&](auto k1) { b[P1 * k1] = v[k1]; });
+  }
+  static __device__ __forceinline__ void read1(float2 (&v)[16], const float2* buf, int t) {
+    const int u = t % L, k1 = t / L;
+    const float2* b = buf + P1 * k1 + u;
+    static_for<0, 16>([&](auto r) { v[r] = b[L * r]; });
+  }
+  static __device__ __forceinline__ void pass2(float2 (&v)[16], float2 w2) {
+    dft16(v);
+    twiddle(v, w2);
+  }
+  static __device__ __forceinline__ void write2(const float2 (&v)[16], float2* buf, int t) {
+    const int u = t % L, k1 = t / L;
+    float2* bw = buf + P2R * k1 + u;
+    static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
+  }
+  static __device__ __forceinline__ void read2(float2 (&v)[16], const float2* buf, int t) {
+    if constexpr (L == 16) {
+      const int k2 = t & 15, k1 = t >> 4;
+      const float2* b = buf + P2R * k1 + P2C * k2;
+      static_for<0, 16>([&](auto r) { v[r] = b[r]; });
+    } else {
+      const int q = t & 1, k2 = (t >> 1) & 15, k1 = t >> 5;
+      const float2* b = buf + P2R * k1 + P2C * k2 + q;
+      static_for<0, 16>([&](auto r) { v[r] = b[2 * r]; });
+    }
+  }
+  static __device__ __forceinline__ void pass3(float2 (&v)[16], int t) {
+    dft16(v);
+    if constexpr (L == 32) {
+      const int q = t & 1;
+      if (q) static_for<1, 16>([&](auto m) { v[m] = twc<m, 32>(v[m]); });
+      const float s = q ? -1.f : 1.f;
+      static_for<0, 16>([&](auto m) {
+        const float px = lane_xor1(v[m].x), py = lane_xor1(v[m].y);
+        v[m] = make_float2(fmaf(v[m].x, s, px), fmaf(v[m].y, s, py));
+      });
+    }
+  }
+
+  // Two frames' forward FFTs (a, b: same plan, same thread roles as run2()) through ONE exchange
+  // buffer, interleaved so that each frame's butterflies fill the other frame's LDS exchange: while
+  // the buffer carries frame a, the waves compute frame b and the other way round. Every buffer use is
+  // write -> barrier -> read -> barrier (the reads done before the other frame writes); the other
+  // frame's pass sits between a write and its barrier (the wave's stores drain and the slower waves
+  // catch up meanwhile). Two frames in flight per workgroup on one 64 KiB buffer: a CU holds four
+  // frames instead of two. SYNC: a barrier before the first write (the buffer may still be read).
+  template <bool SYNC = false>
+  static __device__ __forceinline__ void run_pair(float2 (&a)[16], float2 (&b)[16], float2* buf, int t1, int t,
+                                                  float2 w1, float2 w2) {
+    pass1(a, w1);
+    if constexpr (SYNC) __syncthreads();
+    write1(a, buf, t1);
+    pass1(b, w1);
+    __syncthreads();
+    read1(a, buf, t);
+    __syncthreads();
+    write1(b, buf, t1);
+    pass2(a, w2);
+    __syncthreads();
+    read1(b, buf, t);
+    __syncthreads();
+    write2(a, buf, t);
+    pass2(b, w2);
+    __syncthreads();
+    read2(a, buf, t);
+    __syncthreads();
+    write2(b, buf, t);
+    pass3(a, t);
+    __syncthreads();
+    read2(b, buf, t);
+    pass3(b, t);
+  }
+
   // Natural-order spectrum exchange after run(): every register to its frequency's slot
   // (the caller synchronises before, if the buffer may still be read, and after).
   static __device__ __forceinline__ void store_spectrum(const float2 (&v)[16], float2* buf, int t) {

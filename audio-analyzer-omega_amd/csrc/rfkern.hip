@@ -21,6 +21,7 @@
 
 namespace omega {
 OMEGA_STAMPS_DECL
+OMEGA_WGTRACE_DECL
 }  // namespace omega
 
 #include "kw.hpp"
@@ -188,7 +189,9 @@ __global__ __launch_bounds__(K / 16, 4) void truepeak_rf_kernel(SpectralParams p
     for (int i = 0; i < OMEGA_TP_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
   }
 #endif
+  OMEGA_WG_BEGIN();
   truepeak_rf_body<K>(p, blockIdx.x, threadIdx.x, smem);
+  OMEGA_WG_END(1);
 }
 
 // Multi-resolution frame body (A3-A5) for one resolution of K = N_r/2 complex points: windowed
@@ -271,13 +274,131 @@ __device__ __forceinline__ void mrfft_rf_body(const SpectralParams& p, int r, in
   for (int e = e0 + NTH; e < rp.ent_end; e += NTH) apply(p.ent[e]);
 }
 
+// Two frames (cfa, cfb) of one resolution through one workgroup and one exchange buffer
+// (RegFFT::run_pair): the same outputs as mrfft_rf_body on each. has_b false: the second slot repeats
+// frame a and stores nothing.
+template <int K>
+__device__ __forceinline__ void mrfft_rf_pair_body(const SpectralParams& p, int r, int64_t cfa, int64_t cfb, bool has_b,
+                                                   int t, char* smem) {
+  using FFT = RegFFT<K>;
+  constexpr int NTH = FFT::NTH;
+  float2* buf = reinterpret_cast<float2*>(smem);
+  const ResParam& rp = p.res[r];
+  auto frame = [&](int64_t cf) {
+    const int64_t f = cf / p.C, c = cf % p.C;
+    return reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride + rp.offset);
+  };
+  const float2* xa = frame(cfa);
+  const float2* xb = frame(has_b ? cfb : cfa);
+  const float2* w2 = reinterpret_cast<const float2*>(rp.win);
+  const float2* __restrict__ twK = p.tw[ilog2(K)];
+  const float2* __restrict__ twM = p.tw[ilog2(2 * K)];
+  float2 a[16], b[16];
+  const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];
+  const float2 wm = twM[t];
+  asm volatile("" ::: "memory");
+  static_for<0, 16>([&](auto q) {
+    const float2 u = xa[t + NTH * q], v = xb[t + NTH * q], w = w2[t + NTH * q];
+    a[q] = make_float2(u.x * w.x, u.y * w.y);
+    b[q] = make_float2(v.x * w.x, v.y * w.y);
+  });
+  FFT::template run_pair<false>(a, b, buf, t, t, w1, w2b);
+  // natural-order spectra one frame at a time through the buffer; |X_k| on the thread's bins
+  float mga[16], mgb[16];
+  float nya = 0.f, nyb = 0.f;
+  auto untangle_mag = [&](const float2 (&v)[16], float (&mg)[16], float& mnyq) {
+    __syncthreads();
+    FFT::store_spectrum(v, buf, t);
+    __syncthreads();
+    const float2* bo = buf + FFT::s3(t);
+    const float2* bm = buf + FFT::s3m(t);
+    static_for<0, 16>([&](auto q) {
+      const float2 x0 = bo[FFT::o3(q)];
+      float2 x1 = bm[FFT::o3(15 - q)];
+      if constexpr (K == 8192 && q == 8) {
+        if (t == 0) x1 = x0;
+      }
+      float2 xk, xkk;
+      untangle(x0, x1, twc<q, 32>(wm), xk, xkk);
+      mg[q] = cabs(xk);
+      if constexpr (q == 0) {
+        if (t == 0) {
+          mg[0] = fabsf(x0.x + x0.y);
+          mnyq = fabsf(x0.x - x0.y);
+        }
+      }
+    });
+  };
+  untangle_mag(a, mga, nya);
+  untangle_mag(b, mgb, nyb);
+  if (rp.mag_out) {
+    const float* __restrict__ wgt = rp.wgt;
+    float* oa = rp.mag_out + cfa * (K + 1);
+    static_for<0, 16>([&](auto q) { oa[t + NTH * q] = mga[q] * wgt[t + NTH * q]; });
+    if (t == 0) oa[K] = nya * wgt[K];
+    if (has_b) {
+      float* ob = rp.mag_out + cfb * (K + 1);
+      static_for<0, 16>([&](auto q) { ob[t + NTH * q] = mgb[q] * wgt[t + NTH * q]; });
+      if (t == 0) ob[K] = nyb * wgt[K];
+    }
+  }
+  if (!p.comb_out) return;
+  // both frames' magnitudes parked side by side (2 (K + 1) floats fit the exchange buffer)
+  float* mag = reinterpret_cast<float*>(smem);
+  __syncthreads();
+  static_for<0, 16>([&](auto q) {
+    mag[t + NTH * q] = mga[q];
+    mag[K + 1 + t + NTH * q] = mgb[q];
+  });
+  if (t == 0) {
+    mag[K] = nya;
+    mag[2 * K + 1] = nyb;
+  }
+  __syncthreads();
+  float* oa = p.comb_out + cfa * p.T;
+  float* ob = p.comb_out + cfb * p.T;
+  auto apply = [&](const CombEnt& en) {
+    const int tt = en.tm & 0xFFFFFF, op = en.tm >> 24;
+    const float va = fmaf(en.c1, mag[en.j + 1], en.c0 * mag[en.j]);
+    const float vb = fmaf(en.c1, mag[K + 1 + en.j + 1], en.c0 * mag[K + 1 + en.j]);
+    if (op == 0) {
+      oa[tt] = va;
+      if (has_b) ob[tt] = vb;
+    } else if (op == 1) {
+      oa[tt] += va;
+      if (has_b) ob[tt] += vb;
+    } else {
+      oa[tt] = 0.f;
+      if (has_b) ob[tt] = 0.f;
+    }
+  };
+  for (int e = rp.ent_begin + t; e < rp.ent_end; e += NTH) apply(p.ent[e]);
+}
+
+template <int K>
+__global__ __launch_bounds__(K / 16, 4) void mrfft_rf_pair_kernel(SpectralParams p, int r) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int64_t cfa = 2 * (int64_t)blockIdx.x, cfb = cfa + 1;
+  OMEGA_WG_BEGIN();
+  mrfft_rf_pair_body<K>(p, r, cfa, cfb, cfb < p.n_cf, threadIdx.x, smem);
+  OMEGA_WG_END(12);
+}
+
 template <int K>
 __global__ __launch_bounds__(K / 16, 4) void mrfft_rf_kernel(SpectralParams p, int r) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  OMEGA_WG_BEGIN();
   mrfft_rf_body<K>(p, r, blockIdx.x, threadIdx.x, smem);
+  OMEGA_WG_END(2);
 }
 
 OMEGA_STAMPS_GETTER(omega_debug_rf_stamps)
+OMEGA_WGTRACE_GETTER(omega_debug_wgtrace)
+
+hipError_t launch_mrfft_rf_pair(const SpectralParams& p, int r, hipStream_t s) {
+  hipLaunchKernelGGL(mrfft_rf_pair_kernel<8192>, dim3((unsigned)((p.n_cf + 1) / 2)), dim3(512), lds_bytes<8192>(), s, p, r);
+  return hipGetLastError();
+}
 
 hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
@@ -696,6 +817,7 @@ __device__ __forceinline__ void batch_tp_meter(const SpectralParams& sp, const B
 __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, char* smem) {
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
+  OMEGA_WG_BEGIN();
 #if OMEGA_BATCH_EXTRAS
   if (b == bp.tpm_wg) {
     batch_tp_meter(sp, bp, tid, smem);
@@ -715,6 +837,7 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
     } else {
       mrfft_rf_body<8192>(sp, bp.mr_res, cf, tid, smem);
     }
+    OMEGA_WG_END(role);
     return;
   }
   const MultiPlan& mp = bp.multi;
@@ -732,6 +855,7 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
     case 8192: batch_multi<4096>(sp, r, wg, tid, buf); break;
     default: break;
   }
+  OMEGA_WG_END(3 + sp.res[r].n);
 }
 
 __global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams sp, KWeightParams kp, BatchPlan bp) {

@@ -8,10 +8,6 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libomega.so")
-if os.environ.get("OMEGA_STAMPS_BUILD") == "1":  # kernel-development build (make stamps), tools/stamps.py
-    LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libomega_stamps.so")
-elif os.environ.get("OMEGA_VARIANT"):  # kernel-development variant (make variant VAR=...)
-    LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", f"var_{os.environ['OMEGA_VARIANT']}.so")
 
 MAX_RES = 4
 N_METERS = 5
@@ -144,6 +140,16 @@ def _share_torch_hip_runtime() -> None:
         if os.path.exists(p):
             C.CDLL(p, mode=C.RTLD_GLOBAL)
             return
+
+
+def use_development_library(name: str) -> None:
+    """Kernel-development tools only (tools/stamps.py, tools/wgtrace.py): load lib/<name> (e.g.
+    libomega_dev.so from `make dev`) instead of libomega.so. Must run before the first lib() call; the
+    product path never calls it and reads no environment variable to pick its library."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("libomega is already loaded")
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", name)
 
 
 def lib() -> C.CDLL:

@@ -1,18 +1,20 @@
 #!/usr/bin/env python3
-"""Phase timings from the timestamp build (make -C audio-analyzer-omega_amd stamps):
-OMEGA_STAMPS_BUILD=1 python tools/stamps.py kw  -- runs the stage on the cfg2 batch and prints, for
+"""Phase timings from the timestamp build (make -C audio-analyzer-omega_amd dev):
+python tools/stamps.py kw  -- runs the stage on the cfg2 batch and prints, for
 workgroups 0..3, each wave's s_memtime stamps relative to the workgroup's first stamp (in units of
 the shader clock)."""
 import ctypes as C
 import os
 import sys
 
-os.environ["OMEGA_STAMPS_BUILD"] = "1"
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "audio-analyzer-omega_amd"))
 sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
+from omega_gpu import _lib as _L  # noqa: E402
+
+_L.use_development_library("libomega_dev.so")
 
 
 def main(stage):
