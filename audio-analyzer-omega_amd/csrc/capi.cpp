@@ -31,14 +31,12 @@ hipError_t launch_mrfft_independent(const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s);
 hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s);
-hipError_t launch_mrfft_rf_pair(const SpectralParams& p, int r, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
 hipError_t launch_weight64(const Weight64Params& p, hipStream_t s);
 hipError_t launch_any(const AnyFftParams& p, int truepeak, hipStream_t s);
 hipError_t launch_spectra(int m, const SpectraParams& p, int grid, hipStream_t s);
 hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s);
-hipError_t launch_frame(const SpectralParams& sp, const KWeightParams& kp, hipStream_t s);
 hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_query(const MeterPrepParams& p, hipStream_t s);
@@ -165,12 +163,6 @@ BiquadTab make_biquad_tab(const BiquadCoef& c, int L) {
     }
     if (n + 1 <= L) mat2_mul(A, An, An);
   }
-  // A^(L / kKwSub) for the sub-chunks of one thread's chunk
-  {
-    double As[4] = {1, 0, 0, 1};
-    for (int n = 0; n < L / kKwSub; ++n) mat2_mul(A, As, As);
-    for (int q = 0; q < 4; ++q) t.psub[q] = (float)As[q];
-  }
   // A^j B, j < L
   {
     double g[2] = {B0, B1};
@@ -215,36 +207,20 @@ struct omega_ctx {
   // put the stream layout's nodes on other queues, with ~12 us cross-queue waits and ~20 us between
   // consecutive launches (cfg2 step 149.5 us vs 128.8 us for direct launches of the same layout)
   bool use_graph = false;
-  // stream layout of the per-batch work (enqueue_frames): 0 sequential, 1 concurrent branches,
-  // 2 sequential full-chip kernels with the meter aggregates on a side stream, 3 (default; 16384-sample
-  // frames, direct launches) one batch_kernel launch for all per-channel-frame work, the meter prep on
-  // the side stream waiting on the batch's K-weighting count (kw_done) instead of a stream event.
-  // (A variant ordered by device flags -- prep kernel's last workgroup stores a sequence number, a
-  // one-wave gate kernel waits for it before the query -- measured 124.9 us/step vs 114.9: the gate
-  // launch costs ~5 us and hipStreamWaitValue32 runs as a spinning blit kernel that holds a CU.)
+  // stream layout of the per-batch work (enqueue_frames): 3 (default; 16384-sample frames, direct
+  // launches) one batch_kernel launch for all per-channel-frame work, the meter prep on the side stream
+  // waiting on the batch's K-weighting count (kw_done) instead of a stream event; 2 (other frame sizes,
+  // graph capture, or omega_set_graphs layout bits) the full-chip kernels back to back with the meter
+  // aggregates on a side stream joined by events.
   int layout = 3;
   unsigned* d_kw_done = nullptr;  // batch_kernel's K-weighting workgroups count themselves in here
   unsigned kw_issued = 0;         // K-weighting workgroups launched with the count on (wraps)
   unsigned q_issued = 0;          // LUFS-meter query workgroups launched with the count on (d_kw_done[1])
-  unsigned p_issued = 0;          // tail layout: meter-prep workgroups launched with the count on (d_kw_done[2])
-  unsigned tp_issued = 0;         // batch true-peak workgroups launched with the count on (d_kw_done[3])
-  unsigned wg_issued = 0;         // batch workgroups launched with the join count on (d_kw_done[4])
-  // the true-peak meter query on the side stream and a join in the batch kernel's last workgroup instead
-  // of the query after the batch (OMEGA_BATCH_JOIN=1): measured slower (85.2-87.3 vs 79.9-81.2 us per
-  // step) -- the query workgroups wait for the true-peak count while resident, each holding the
-  // registers of half a batch workgroup slot
-  bool batch_join = false;
-  // the true-peak meter as the batch grid's last workgroup instead of a kernel after the batch
-  // (OMEGA_TP_METER_BATCH=1; one meter chunk): parity green, measured slower (86-88 vs 80-83 us per
-  // step, the window maxima per thread or staged in LDS alike)
-  bool tp_meter_in_batch = false;
-  bool meter_tail = false;        // tail layout: prep alone beside the batch, both query parts after it
   // device-side poll expiry flags (host-mapped: [0] meter prep, [1] join), checked by
   // check_device_err; the poll bound (OMEGA_POLL_LIMIT, a test knob)
   unsigned* h_err = nullptr;
   unsigned* d_err = nullptr;
   int poll_limit = 1 << 22;
-  int batch_order = 3;            // role order of the batch launch (enqueue_batch; OMEGA_BATCH_ORDER)
   bool res_independent = false;  // no combine target has several owners: resolution kernels commute
   hipEvent_t ev_kw = nullptr;
   struct GraphEntry {
@@ -256,8 +232,6 @@ struct omega_ctx {
   char err[512] = {};  // omega_last_error (a fixed buffer: reporting an error allocates nothing)
   // tables
   float2* d_tw[kMaxLog2] = {};
-  float4* d_rtw1[2] = {};  // register-FFT twiddle tables (build_rf_twiddles), K = 4096 / 8192
-  float4* d_rtw2[2] = {};
 
   float2* d_rot = nullptr;
   float* d_win[kMaxRes] = {};
@@ -265,13 +239,7 @@ struct omega_ctx {
   CombEnt* d_ent = nullptr;
   int ent_begin[kMaxRes] = {}, ent_end[kMaxRes] = {};
   std::map<std::pair<int, int>, BiquadTab*> kw_tabs;  // (M, chunk) -> device {hp, shelf}
-  float4* d_tpx = nullptr;  // true-peak spectrum scratch (16384-sample frames), tpx_cap channel-frames
-  int64_t tpx_cap = 0;
-  bool tp_l2 = false;       // 512-thread true peak with the spectrum in L2 (OMEGA_TP_L2=1; measured slower)
-  bool fuse_frame = false;  // W = 16384: K-weighting + true peak in one kernel (OMEGA_FUSE=1 enables)
-  int rf_sizes = 1 << 14;   // resolution sizes on the register-FFT kernel (OMEGA_RF_SIZES bit mask)
-  bool spectra_rf = true;   // register-FFT cfg3 spectra kernel for 8192-point frames (OMEGA_SPECTRA_RF=0: old)
-  bool tp_rf = true;        // register-FFT true peak for W = 8192 / 16384 (OMEGA_TP_RF=0: the LDS-pass kernel)
+  int rf_sizes = 1 << 14;   // resolution sizes on the register-FFT kernel (bit log2 N): the 16384-point one
   std::map<std::pair<int, int>, float*> windows;  // (m, kind) -> device window
   std::map<int, float2*> rots;                     // m -> true-peak rotation table
   // combine plan as per-target owner lists (CSR) for omega_combine over a subset of resolutions
@@ -544,61 +512,12 @@ void drop_graphs(omega_ctx* c) {
   c->graphs.clear();
 }
 
-// True-peak kernel choice: the register-FFT kernel for 8192- and 16384-sample frames (unless
-// OMEGA_TP_RF=0 or the L2-scratch variant is selected), otherwise the LDS-pass kernel.
+// True-peak kernel choice: the register-FFT kernel for 8192- and 16384-sample frames, the LDS-pass
+// kernel for the other powers of two.
 hipError_t tp_launch(omega_ctx* c, int W, const SpectralParams& sp, hipStream_t s) {
-  if (c->tp_rf && !sp.tp_scratch && (W == 16384 || W == 8192)) return launch_truepeak_rf(W, sp, s);
+  (void)c;
+  if (W == 16384 || W == 8192) return launch_truepeak_rf(W, sp, s);
   return launch_truepeak(W, sp, s);
-}
-
-// Spectrum scratch of the 512-thread true-peak kernel (W = 16384): 64 KiB per channel-frame, grown
-// on demand up to 8192 channel-frames (larger calls use the register-resident kernel). Growing
-// drops the captured graphs, which hold the old pointer.
-int tp_scratch(omega_ctx* c, int W, int64_t n_cf, float4** out) {
-  *out = nullptr;
-  if (W != 16384 || !c->tp_l2 || n_cf > 8192) return 0;
-  if (n_cf > c->tpx_cap) {
-    const int64_t cap = std::max<int64_t>(n_cf, 512);
-    if (c->d_tpx) {
-      HIPC(c, hipDeviceSynchronize());
-      (void)hipFree(c->d_tpx);
-      c->d_tpx = nullptr;
-      c->tpx_cap = 0;
-    }
-    drop_graphs(c);
-    HIPC(c, hipMalloc(&c->d_tpx, (size_t)cap * (W / 4) * sizeof(float4)));
-    c->tpx_cap = cap;
-  }
-  *out = c->d_tpx;
-  return 0;
-}
-
-// Register-FFT inter-pass twiddle tables (regfft.hpp RegFFT::run): for K = 4096 and 8192 points,
-// rtw1[j * NTH + t] = (W^{t (2j+1)}, W^{t (2j+2)}) and rtw2[j * L + u] = (W^{16u (2j+1)}, W^{16u (2j+2)}),
-// W = e^{-2 pi i / K}, j < 8 (float64 angles rounded once to float32).
-int build_rf_twiddles(omega_ctx* c) {
-  for (int i = 0; i < 2; ++i) {
-    const int K = i ? 8192 : 4096, NTH = K / 16, L = K / 256;
-    auto w = [&](long long m) {
-      const double a = -2.0 * M_PI * (double)(m % K) / K;
-      return std::make_pair((float)std::cos(a), (float)std::sin(a));
-    };
-    std::vector<float4> t1((size_t)8 * NTH), t2((size_t)8 * L);
-    for (int j = 0; j < 8; ++j) {
-      for (int t = 0; t < NTH; ++t) {
-        const auto a = w((long long)t * (2 * j + 1)), b = w((long long)t * (2 * j + 2));
-        t1[(size_t)j * NTH + t] = make_float4(a.first, a.second, b.first, b.second);
-      }
-      for (int u = 0; u < L; ++u) {
-        const auto a = w(16LL * u * (2 * j + 1)), b = w(16LL * u * (2 * j + 2));
-        t2[(size_t)j * L + u] = make_float4(a.first, a.second, b.first, b.second);
-      }
-    }
-    int e = upload(c, &c->d_rtw1[i], t1);
-    if (!e) e = upload(c, &c->d_rtw2[i], t2);
-    if (e) return e;
-  }
-  return 0;
 }
 
 int build_spectral_tables(omega_ctx* c) {
@@ -755,7 +674,7 @@ int build_meter_state(omega_ctx* c) {
     HIPC(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_err), c->h_err, 0));
   }
   HIPC(c, hipMemset(c->d_kw_done, 0, 8 * sizeof(unsigned)));
-  c->kw_issued = c->q_issued = c->p_issued = c->tp_issued = c->wg_issued = 0;
+  c->kw_issued = c->q_issued = 0;
   return omega_meter_reset(c);
 }
 
@@ -765,10 +684,6 @@ SpectralParams spectral_params(omega_ctx* c) {
   p.C = c->cfg.n_channels;
   p.n_res = c->cfg.n_res;
   p.rf_sizes = c->rf_sizes;
-  for (int i = 0; i < 2; ++i) {
-    p.rtw1[i] = c->d_rtw1[i];
-    p.rtw2[i] = c->d_rtw2[i];
-  }
   for (int r = 0; r < p.n_res; ++r) {
     ResParam& q = p.res[r];
     q.n = c->cfg.res[r].fft_size;
@@ -896,7 +811,7 @@ int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_f
 bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, bool do_res, hipStream_t s,
                     int* mr) {
   *mr = -1;
-  if (W != 16384 || s == c->cap || c->fuse_frame || sp.tp_scratch || !c->tp_rf) return false;
+  if (W != 16384 || s == c->cap) return false;
   if ((kp.lufs_out || kp.weighted_out) && kp.mode != 0) return false;
   if (!do_res) return true;
   if (!c->res_independent) return false;
@@ -913,37 +828,29 @@ bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams&
   return true;
 }
 
-// The default layout for 16384-sample frames (c->batch_order 3). On `s`: one batch_kernel launch
-// (BatchPlan: K-weighting and 16384-point-resolution workgroups mixed, then the true peaks, then the
-// small resolutions) and the true-peak meter. On fork[0]: the meter prep (it waits on the K-weighting
-// count, kw_done) and the LUFS meters (their workgroups count themselves in). The true-peak meter's
-// first workgroup waits for that count, so `s` completes only after fork[0]'s work: no stream events
-// anywhere (each event record / wait cost ~7-13 us of idle GPU between kernels). cfg2 step on MI355X:
-// 79.5 us (order 3); 85.2 (2: K-weighting mixed with the true peaks), 110.4 (0: K-weighting as its own
-// kernel first: it mixes with nothing); 4 (the true peaks first, then K-weighting mixed with the
-// 16384-point resolution) the same as 3 within noise (81.2 vs 80.9 us per call); the side-meter
-// layout with events 99.2. Mixing the
-// latency-bound K-weighting scans with transform work is what pays (K-weighting alone 25.7 us, the
-// true peak 37, the resolutions 26.5; one batch launch of all three 73.9).
+// The default layout for 16384-sample frames. On `s`: one batch_kernel launch (BatchPlan: K-weighting
+// and 16384-point-resolution workgroups mixed, then the true peaks, then the small resolutions) and the
+// true-peak meter. On fork[0]: the meter prep (it waits on the K-weighting count, kw_done) and the LUFS
+// meters (their workgroups count themselves in). The true-peak meter's first workgroup waits for that
+// count, so `s` completes only after fork[0]'s work: no stream events anywhere (each event record /
+// wait cost ~7-13 us of idle GPU between kernels). Mixing the latency-bound K-weighting scans with
+// transform work is what pays (K-weighting alone 25.7 us, the true peak 37, the resolutions 26.5; one
+// batch launch of all three 73.9). Measured and rejected on MI355X (round 1-2): other role
+// orders (K-weighting as its own kernel 110.4 us per step; mixed with the true peaks 85.2; the true
+// peaks first ~equal), the meter queries after the batch (88 vs 81-82), the true-peak query on the side
+// stream joined in the batch's last workgroup (85-87), the true-peak meter as a batch role (86-88).
 int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
                   const float* tp, double* meters, hipStream_t s, int mr, bool do_tp, bool do_kw) {
+  (void)W;
   const int64_t n = sp.n_cf;
-  const int order = c->batch_order;
-  const bool kw_in_batch = do_kw && order != 0;
   BatchPlan bp{};
   int seg[2][3], ns[2] = {0, 0};
   auto add = [&](int sg, int role, bool on) {
     if (on) seg[sg][ns[sg]++] = role;
   };
-  if (order == 4) {  // the true peaks first, then K-weighting mixed with the 16384-point resolution
-    add(0, 1, do_tp);
-    add(1, 0, kw_in_batch);
-    add(1, 2, mr >= 0);
-  } else {
-    add(0, 0, kw_in_batch);
-    add(order == 1 || order == 2 ? 0 : 1, 1, do_tp);
-    add(order == 1 || order == 3 ? 0 : 1, 2, mr >= 0);
-  }
+  add(0, 0, do_kw);        // segment 0: K-weighting and the 16384-point resolution, groups of 8 frames
+  add(0, 2, mr >= 0);
+  add(1, 1, do_tp);        // segment 1: the true peaks
   const int64_t groups = (n + 7) / 8;
   int64_t end = 0;
   for (int sg = 0; sg < 2; ++sg) {
@@ -968,24 +875,11 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   const int64_t grid = end + nwg;
   if (grid > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
   std::vector<MeterPrepParams> mc;
-  bool tail = false;
   if (meters) {
     mc = meter_chunks(c, lufs, tp, n_frames, meters);
     kp.kw_done = c->d_kw_done;
     c->kw_issued += (unsigned)n;
-    // tail layout (one meter chunk: a second chunk's prep would overwrite the per-batch scratch before
-    // the first chunk's query ran): the prep waits for the K-weighting count beside the batch and counts
-    // itself in; both query parts run after the batch on `s`
-    tail = c->meter_tail && mc.size() == 1;
-    if (tail) {
-      MeterPrepParams p = mc[0];
-      p.wait_ctr = c->d_kw_done;
-      p.wait_target = c->kw_issued;
-      p.q_done = c->d_kw_done + 2;
-      HIPC(c, launch_meter_prep(p, c->fork[0]));
-      c->p_issued += (unsigned)p.C;
-    }
-    for (size_t i = 0; i < mc.size() && !tail; ++i) {
+    for (size_t i = 0; i < mc.size(); ++i) {
       MeterPrepParams p = mc[i];
       if (i == 0) {
         p.wait_ctr = c->d_kw_done;
@@ -998,78 +892,14 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
       c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);  // (counted once it is enqueued)
     }
   }
-  // the join (default): the true-peak meter queries follow on the side stream (the first waits for the
-  // batch's true-peak count) and the batch kernel's last workgroup waits for every query workgroup, so
-  // `s` ends with the batch kernel (no kernel after it on the critical path)
-  const bool join = kBatchExtras && meters && !tail && c->batch_join && do_tp && grid > 0;
-  // (the role stages history ++ batch of one channel in the batch kernel's LDS)
-  const bool tpm = kBatchExtras && meters && !tail && !join && c->tp_meter_in_batch && do_tp && grid > 0 && mc.size() == 1 &&
-                   (size_t)(mc[0].HT + mc[0].n_frames) * sizeof(float) <= 65536;
-  int64_t grid_all = grid;
-#if OMEGA_BATCH_EXTRAS
-  bp.tpm_wg = -1;
-#endif
-  if (tpm) {
-#if OMEGA_BATCH_EXTRAS
-    sp.tp_done = c->d_kw_done + 3;
-    c->tp_issued += (unsigned)n;
-    bp.tpm_wg = (int)grid;
-    bp.tp_target = c->tp_issued;
-    bp.mq = mc[0];
-    bp.join_ctr = c->d_kw_done + 1;
-    bp.join_target = c->q_issued;
-    bp.poll_limit = c->poll_limit;
-    bp.err_word = c->d_err;
-    grid_all = grid + 1;
-#endif
-  }
-  if (join) {
-    sp.tp_done = c->d_kw_done + 3;
-    c->tp_issued += (unsigned)n;
-    for (size_t i = 0; i < mc.size(); ++i) {
-      MeterPrepParams p = mc[i];
-      p.parts = 2;
-      p.q_done = c->d_kw_done + 1;
-      if (i == 0) {
-        p.start_ctr = c->d_kw_done + 3;
-        p.start_target = c->tp_issued;
-      }
-      HIPC(c, launch_meter_query(p, c->fork[0]));
-      c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);
-    }
-    c->wg_issued += (unsigned)grid;
-#if OMEGA_BATCH_EXTRAS
-    bp.wg_done = c->d_kw_done + 4;
-    bp.wg_target = c->wg_issued;
-    bp.join_ctr = c->d_kw_done + 1;
-    bp.join_target = c->q_issued;
-    bp.poll_limit = c->poll_limit;
-    bp.err_word = c->d_err;
-#endif
-  }
-  {
-    hipError_t le = hipSuccess;
-    if (do_kw && !kw_in_batch) le = launch_kweight(W, kp, s);
-    if (le == hipSuccess && grid > 0) le = launch_batch(sp, kp, bp, (int)grid_all, s);
+  if (grid > 0) {
+    const hipError_t le = launch_batch(sp, kp, bp, (int)grid, s);
     if (le != hipSuccess) {
       // the prep kernel already waits for this batch's count: publish it, so that it (and every later
       // call's target) stays in step with the device counter instead of timing out
       if (meters) (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
-      if (join || tpm) {  // the same for the side stream's true-peak query and the join count
-        (void)hipMemcpy(c->d_kw_done + 3, &c->tp_issued, sizeof(unsigned), hipMemcpyHostToDevice);
-        (void)hipMemcpy(c->d_kw_done + 4, &c->wg_issued, sizeof(unsigned), hipMemcpyHostToDevice);
-      }
       return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
     }
-  }
-  if (join || tpm) return 0;
-  if (tail) {
-    MeterPrepParams p = mc[0];
-    p.parts = 3;
-    p.start_ctr = c->d_kw_done + 2;
-    p.start_target = c->p_issued;
-    HIPC(c, launch_meter_query(p, s));
-    return 0;
   }
   for (size_t i = 0; i < mc.size(); ++i) {
     MeterPrepParams p = mc[i];
@@ -1083,89 +913,39 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   return 0;
 }
 
-// The per-batch work (c->layout). 0 sequential: resolution kernels, true peak, K-weighting, meters on
-// `s`. 1 concurrent: true peak on fork[1] and the resolution kernels (in resolution order) on fork[0]
-// from the start; K-weighting and then the meter aggregates' prep kernel (it needs the batch's
-// LUFS_inst only) on `s`, whose query kernel then waits for the true peaks; both branches join back
-// into `s`. 2 (default): see below.
-// kp16: the K-weighting parameters with 16-sample-chunk tables for the fused frame kernel (hp null
-// when not built).
-int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, const KWeightParams& kp16, int W,
-                   int64_t n_frames, const float* lufs, const float* tp, double* meters, hipStream_t s) {
+// The per-batch work: layout 3 (enqueue_batch) where eligible, otherwise the full-chip kernels back to
+// back on `s` (K-weighting first); the meter aggregates' prep and LUFS query kernels (one or two
+// workgroups per channel: latency-bound) run on fork[0] beside the resolution and true-peak kernels,
+// the true-peak meter after the true peaks on `s`. (Concurrent full-chip kernels lose to this: 512
+// channel-frames are exactly two rounds of 256 CUs, and a CU held by another kernel pushes a third.)
+int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, int64_t n_frames,
+                   const float* lufs, const float* tp, double* meters, hipStream_t s) {
   const bool do_tp = sp.tp_out != nullptr, do_kw = kp.lufs_out || kp.weighted_out;
   const bool do_res = sp.comb_out != nullptr || sp.res[0].mag_out || sp.res[1].mag_out || sp.res[2].mag_out ||
                       sp.res[3].mag_out;
   int mr = -1;
   if (c->layout == 3 && batch_eligible(c, sp, kp, W, do_res, s, &mr))
     return enqueue_batch(c, sp, kp, W, n_frames, lufs, tp, meters, s, mr, do_tp, do_kw);
-  const int layout = c->layout == 3 ? 2 : c->layout;
-  if (layout == 0) {
-    if (do_res) HIPC(c, c->res_independent ? launch_mrfft_independent(sp, s) : launch_mrfft(sp, s));
-    if (do_tp) HIPC(c, tp_launch(c, W, sp, s));
-    if (do_kw) HIPC(c, launch_kweight(W, kp, s));
-    return meters ? meters_enqueue(c, lufs, tp, n_frames, meters, s, nullptr) : 0;
-  }
-  HIPC(c, hipEventRecord(c->ev_fork, s));
-  if (W == 16384 && do_tp && do_kw && kp16.hp && c->fuse_frame) {
-    // fused layout: true peak + K-weighting in one kernel on `s`, then the meters; resolutions on fork[0]
-    if (do_res) {
-      HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
-      HIPC(c, c->res_independent ? launch_mrfft_independent(sp, c->fork[0]) : launch_mrfft(sp, c->fork[0]));
-      HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
-    }
-    HIPC(c, launch_frame(sp, kp16, s));
-    if (meters) {
-      const int e = meters_enqueue(c, lufs, tp, n_frames, meters, s, nullptr);
-      if (e) return e;
-    }
-    if (do_res) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
-    return 0;
-  }
-  if (layout == 2) {
-    // the full-chip kernels back to back on `s` (K-weighting first); the meter aggregates' prep and
-    // LUFS query kernels (one or two workgroups per channel: latency-bound) run on fork[0] beside the
-    // resolution and true-peak kernels, the true-peak meter after the true peaks on `s`. (Concurrent
-    // full-chip kernels lose to this: 512 channel-frames are exactly two rounds of 256 CUs, and a CU
-    // held by another kernel pushes a third round.)
-    if (do_kw) HIPC(c, launch_kweight(W, kp, s));
-    std::vector<MeterPrepParams> mc;
-    if (meters) {
-      mc = meter_chunks(c, lufs, tp, n_frames, meters);
-      HIPC(c, hipEventRecord(c->ev_kw, s));
-      HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_kw, 0));
-      for (MeterPrepParams p : mc) {
-        HIPC(c, launch_meter_prep(p, c->fork[0]));
-        p.parts = 1;
-        HIPC(c, launch_meter_query(p, c->fork[0]));
-      }
-      HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
-    }
-    if (do_res) HIPC(c, c->res_independent ? launch_mrfft_independent(sp, s) : launch_mrfft(sp, s));
-    if (do_tp) HIPC(c, tp_launch(c, W, sp, s));
+  if (do_kw) HIPC(c, launch_kweight(W, kp, s));
+  std::vector<MeterPrepParams> mc;
+  if (meters) {
+    mc = meter_chunks(c, lufs, tp, n_frames, meters);
+    HIPC(c, hipEventRecord(c->ev_kw, s));
+    HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_kw, 0));
     for (MeterPrepParams p : mc) {
-      p.parts = 2;
-      HIPC(c, launch_meter_query(p, s));
+      HIPC(c, launch_meter_prep(p, c->fork[0]));
+      p.parts = 1;
+      HIPC(c, launch_meter_query(p, c->fork[0]));
     }
-    if (meters) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
-    return 0;
-  }
-  if (do_tp) {
-    HIPC(c, hipStreamWaitEvent(c->fork[1], c->ev_fork, 0));
-    HIPC(c, tp_launch(c, W, sp, c->fork[1]));
-    HIPC(c, hipEventRecord(c->ev_join[1], c->fork[1]));
-  }
-  if (do_res) {
-    HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
-    HIPC(c, c->res_independent ? launch_mrfft_independent(sp, c->fork[0]) : launch_mrfft(sp, c->fork[0]));
     HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
   }
-  if (do_kw) HIPC(c, launch_kweight(W, kp, s));
-  if (meters) {
-    const int e = meters_enqueue(c, lufs, tp, n_frames, meters, s, do_tp ? c->ev_join[1] : nullptr);
-    if (e) return e;
+  if (do_res) HIPC(c, c->res_independent ? launch_mrfft_independent(sp, s) : launch_mrfft(sp, s));
+  if (do_tp) HIPC(c, tp_launch(c, W, sp, s));
+  for (MeterPrepParams p : mc) {
+    p.parts = 2;
+    HIPC(c, launch_meter_query(p, s));
   }
-  if (do_tp) HIPC(c, hipStreamWaitEvent(s, c->ev_join[1], 0));
-  if (do_res) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
+  if (meters) HIPC(c, hipStreamWaitEvent(s, c->ev_join[0], 0));
   return 0;
 }
 
@@ -1179,11 +959,11 @@ const char* omega_version(void) { return "omega-mi355x 0.1 (gfx950, ABI 1)"; }
 // Development build only (make dev): one kernel variant over n_cf channel-frames of the context's
 // frames x (device memory, frame stride W, channel stride W * ... as omega_process_frames with
 // frame_stride = C * W, channel_stride = W), outputs to device buffers. which: 0 the 16384-point
-// resolution single-frame kernel, 1 its two-frames-per-workgroup form (combine of resolution 0);
-// 2 the true-peak kernel (aux: [n_cf] true peaks). (A two-frames-per-workgroup true peak, its spectrum
-// parked in L2 scratch between phases, measured no faster at 8192 channel-frames: 614 vs 621 us, the
-// shader clock 1773 vs 1897 MHz -- the extra frames in flight bought activity, and the clock gave it
-// back.)
+// resolution kernel, 2 the true-peak kernel (aux: [n_cf] true peaks). (Two frames per workgroup
+// through one exchange buffer -- the 16384-point resolution interleaved, and a true peak with its
+// spectrum parked in L2 between phases -- measured no faster at 8192 channel-frames (true peak 614 vs
+// 621 us at a shader clock of 1773 vs 1897 MHz): the extra frames in flight bought activity and the
+// clock gave it back; both were deleted.)
 int omega_dev_probe(omega_ctx* c, int which, const float* x, int64_t n_frames, float* comb, float* aux) {
   SpectralParams sp = spectral_params(c);
   const int W = c->cfg.frame_size;
@@ -1200,7 +980,6 @@ int omega_dev_probe(omega_ctx* c, int which, const float* x, int64_t n_frames, f
   if (int r = get_rot(c, W, &rot)) return r;
   sp.rot = rot;
   if (which == 0) e = launch_mrfft_rf(16384, sp, 0, c->stream);
-  if (which == 1) e = launch_mrfft_rf_pair(sp, 0, c->stream);
   if (which == 2) e = launch_truepeak_rf(16384, sp, c->stream);
   return e == hipSuccess ? 0 : fail(c, OMEGA_EHIP, "probe %d: %s", which, hipGetErrorString(e));
 }
@@ -1248,28 +1027,15 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) try {
     return fail(c, OMEGA_EHIP, "device %d: %s", device, hipGetErrorString(he));
   }
   c->stream = c->own;
-  if (const char* fz = std::getenv("OMEGA_FUSE")) c->fuse_frame = std::atoi(fz) != 0;
-  if (const char* tl = std::getenv("OMEGA_TP_L2")) c->tp_l2 = std::atoi(tl) != 0;
-  if (const char* tr = std::getenv("OMEGA_TP_RF")) c->tp_rf = std::atoi(tr) != 0;
-  if (const char* sr = std::getenv("OMEGA_SPECTRA_RF")) c->spectra_rf = std::atoi(sr) != 0;
-  if (const char* rs = std::getenv("OMEGA_RF_SIZES")) c->rf_sizes = std::atoi(rs) & ((1 << 14) | (1 << 13));
-  if (const char* gr = std::getenv("OMEGA_GRAPHS")) c->use_graph = std::atoi(gr) != 0;
-  if (const char* bo = std::getenv("OMEGA_BATCH_ORDER")) c->batch_order = std::atoi(bo);
-  if (const char* mt = std::getenv("OMEGA_METER_TAIL")) c->meter_tail = std::atoi(mt) != 0;
-  if (const char* bj = std::getenv("OMEGA_BATCH_JOIN")) c->batch_join = std::atoi(bj) != 0;
-  if (const char* tb = std::getenv("OMEGA_TP_METER_BATCH")) c->tp_meter_in_batch = std::atoi(tb) != 0;
+  // the one environment variable the library reads: the device-wait bound of the meter ordering
+  // (a test knob: tests/test_gpu_parity.py test_meter_ordering_expiry_is_reported)
   if (const char* pl = std::getenv("OMEGA_POLL_LIMIT")) c->poll_limit = std::atoi(pl) > 0 ? std::atoi(pl) : 1;
-  if (const char* lay = std::getenv("OMEGA_LAYOUT")) {
-    const int v = std::atoi(lay);
-    c->layout = v < 0 || v > 3 ? 3 : v;
-  }
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking);
   if (he == hipSuccess) {
     // fork[0] carries the latency-bound meter kernels beside full-chip work: at the highest stream
-    // priority (OMEGA_METER_PRIO=0: default priority) a freed CU goes to them first
+    // priority a freed CU goes to them first
     int lo = 0, hi = 0;
-    const char* mp = std::getenv("OMEGA_METER_PRIO");
-    if ((!mp || std::atoi(mp) != 0) && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
       he = hipStreamCreateWithPriority(&c->fork[0], hipStreamNonBlocking, hi);
     else
       he = hipStreamCreateWithFlags(&c->fork[0], hipStreamNonBlocking);
@@ -1285,7 +1051,6 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) try {
   }
   e = build_twiddles(c);
   if (!e) e = build_spectral_tables(c);
-  if (!e) e = build_rf_twiddles(c);
   if (!e) e = build_meter_state(c);
   *out = c;
   return e;
@@ -1726,7 +1491,6 @@ void omega_destroy(omega_ctx* c) try {
   for (DevBuf& b : c->stage)
     if (b.p) (void)hipFree(b.p);
   drop_graphs(c);
-  if (c->d_tpx) (void)hipFree(c->d_tpx);
   if (c->h_err) (void)hipHostFree(c->h_err);
   for (hipStream_t st : {c->cap, c->fork[0], c->fork[1]})
     if (st) (void)hipStreamDestroy(st);
@@ -1759,10 +1523,9 @@ int omega_get_config(const omega_ctx* c, omega_config* cfg, int* device) {
 int omega_set_graphs(omega_ctx* c, int enable) try {
   if (!c) return OMEGA_EINVAL;
   c->use_graph = (enable & 1) != 0;
-  // bits 1-2: 0 default (one batch launch where eligible, else 3), 1 sequential, 2 concurrent
-  // branches, 3 full-chip kernels back to back with the meters on a side stream
-  const int lay = (enable >> 1) & 3;
-  c->layout = lay == 1 ? 0 : (lay == 2 ? 1 : (lay == 3 ? 2 : 3));
+  // bits 1-2: 0 default (one batch launch where eligible), else the full-chip kernels back to back with
+  // the meters on a side stream
+  c->layout = ((enable >> 1) & 3) ? 2 : 3;
   drop_graphs(c);
   return 0;
 } catch (...) {
@@ -1808,10 +1571,6 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
   sp.frame_stride = frame_stride;
   sp.chan_stride = channel_stride;
   sp.n_cf = ncf;
-  if (out->true_peak_db) {
-    const int e0 = tp_scratch(c, W, ncf, &sp.tp_scratch);
-    if (e0) return e0;
-  }
   std::vector<HostOut> outs;
   const float* dx = x;
   float* tp = out->true_peak_db;
@@ -1855,15 +1614,6 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
     if (e) return e;
   }
   KWeightParams kp{dx, frame_stride, channel_stride, C, ncf, tabs, tabs ? tabs + 1 : nullptr, lufs, weighted, 0};
-  KWeightParams kp16 = kp;
-  kp16.hp = kp16.shelf = nullptr;
-  if (tabs && W == 16384 && tp && c->fuse_frame) {
-    BiquadTab* t16 = nullptr;
-    e = get_kw_tab(c, W, kFrameChunk, &t16);
-    if (e) return e;
-    kp16.hp = t16;
-    kp16.shelf = t16 + 1;
-  }
   if (mem == OMEGA_MEM_DEVICE && c->use_graph) {
     // replay a captured graph of this exact call (pointers, sizes, meter-state parity), capturing it on
     // first use: removes the per-launch host cost and runs the three branches concurrently
@@ -1884,7 +1634,7 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
       }
       const int cur0 = c->cur;
       HIPC(c, hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
-      e = enqueue_frames(c, sp, kp, kp16, W, n_frames, lufs, tp, meters, c->cap);
+      e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->cap);
       hipGraph_t graph = nullptr;
       const hipError_t ce = hipStreamEndCapture(c->cap, &graph);
       if (e) return e;
@@ -1897,7 +1647,7 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
     if (meters) c->cur ^= (int)(((n_frames + kChunkFrames - 1) / kChunkFrames) & 1);
     return 0;
   }
-  e = enqueue_frames(c, sp, kp, kp16, W, n_frames, lufs, tp, meters, c->stream);
+  e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->stream);
   if (e) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
@@ -2062,7 +1812,6 @@ int omega_true_peak_os(omega_ctx* c, const float* x, int64_t n, int32_t m, int32
   sp.tp_out = dout;
   float2* rot = nullptr;
   e = get_rot(c, m, &rot);
-  if (!e) e = tp_scratch(c, m, n, &sp.tp_scratch);
   if (e) return e;
   sp.rot = rot;
   sp.tp_phases = oversampling == 4 ? 0xE : (oversampling == 2 ? 0x4 : 0);
@@ -2509,12 +2258,10 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
   p.cperm = c->ctab.perm;
   p.cgoff = c->ctab.goff;
   p.crec = c->ctab.rec;
-  p.rtw1 = c->d_rtw1[0];
-  p.rtw2 = c->d_rtw2[0];
   p.chroma_out = dcr;
   for (int l = 0; l < kMaxLog2; ++l) p.tw[l] = c->d_tw[l];
   const int grid = (int)std::min<int64_t>(n, 2 * (int64_t)c->n_cu);
-  if (c->spectra_rf && m == 8192)
+  if (m == 8192)
     HIPC(c, launch_spectra_rf(m, p, c->stream));
   else
     HIPC(c, launch_spectra(m, p, grid, c->stream));

@@ -1,5 +1,5 @@
-// K-weighting device code (A6/A7), shared by kweight_kernel (kweight.hip) and the fused frame
-// kernel (frame.hip). See kweight.hip for the algorithm. Include after OMEGA_STAMPS_DECL.
+// K-weighting device code (A6/A7), shared by kweight_kernel (kweight.hip) and the batch kernel's
+// K-weighting role (rfkern.hip). See kweight.hip for the algorithm. Include after OMEGA_STAMPS_DECL.
 #pragma once
 #include "fft.hpp"
 #include "params.hpp"
@@ -12,7 +12,6 @@ namespace omega {
 struct BqRegs {
   float b0, a1, a2, B0, B1, zi0, zi1;
   float4 p1, p2, p4, p8, p64;  // P, P^2, P^4, P^8, P^64
-  float4 ps;                   // A^(L / kKwSub)
 };
 
 __device__ __forceinline__ float4 ld4(const float* q) { return make_float4(q[0], q[1], q[2], q[3]); }
@@ -31,7 +30,6 @@ __device__ __forceinline__ BqRegs bq_regs(const BiquadTab* __restrict__ t) {
   r.p4 = ld4(t->pw[3]);
   r.p8 = ld4(t->pw[7]);
   r.p64 = ld4(t->pw[63]);
-  r.ps = ld4(t->psub);
   return r;
 }
 
@@ -82,59 +80,22 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
   const int lane = tid & 63, wv = tid >> 6;
   const int vl = REV ? 63 - lane : lane;       // position in processing order within the wave
   const int vw = REV ? NW - 1 - wv : wv;       // wave position in processing order
-  // 1) zero-state end state of the chunk (outputs come in step 5): kKwSub sub-chunks of LS samples
-  // run interleaved from zero (independent chains), then folded in processing order with A^LS
-  constexpr int S = (L % kKwSub == 0 && L >= 2 * kKwSub) ? kKwSub : 1;
-  constexpr int LS = L / S;
-  float e0[S], e1[S];
-  static_for<0, S>([&](auto j) {
-    e0[j] = 0.f;
-    e1[j] = 0.f;
-  });
-  if constexpr (kKwZtab && !kKwCorr) {
-    // e = sum_i A^(LS-1-i) B u_i over the sub-chunk's samples in processing order: two independent
-    // dot products per sub-chunk (split in halves for shorter FMA chains); the coefficients are LDS
-    // broadcast reads (pwl[64 + j].zw)
-    float f0[S], f1[S];
-    static_for<0, S>([&](auto j) {
-      f0[j] = 0.f;
-      f1[j] = 0.f;
-    });
+  // 1) zero-state end state of the chunk (outputs come in step 5): e = sum_i A^(L-1-i) B u_i over the
+  // chunk's samples in processing order -- two independent dot products whose coefficients are LDS
+  // broadcast reads (pwl[64 + j].zw), instead of the serial state recurrence (4 dependent VALU ops per
+  // sample)
+  float s0 = 0.f, s1 = 0.f;
+  {
     const float2* gt = reinterpret_cast<const float2*>(pwl + 64) + 1;  // (g0, g1) of A^j B at gt[2 j]
-    static_for<0, LS>([&](auto i) {
-      // (groups of 4 broadcast reads: not all hoisted ahead into registers at once)
+    static_for<0, L>([&](auto i) {
+      // (groups of 32 broadcast reads: not all hoisted ahead into registers at once)
       if constexpr (i % 32 == 0) asm volatile("" ::: "memory");
-      const float2 cg = gt[2 * (LS - 1 - i)];
-      const float c0 = cg.x, c1 = cg.y;
-      static_for<0, S>([&](auto j) {
-        constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
-        e0[j] = fmaf(c0, u[n], e0[j]);
-        e1[j] = fmaf(c1, u[n], e1[j]);
-      });
-    });
-    static_for<0, S>([&](auto j) {
-      e0[j] += f0[j];
-      e1[j] += f1[j];
-    });
-  } else {
-    static_for<0, LS>([&](auto i) {
-      static_for<0, S>([&](auto j) {
-        // sub-chunk j in processing order covers samples (REV: from the end) j*LS .. j*LS + LS - 1
-        constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
-        if constexpr (kKwCorr)
-          u[n] = bq_step(t, u[n], e0[j], e1[j]);  // zero-state outputs, corrected in step 5
-        else
-          bq_state(t, u[n], e0[j], e1[j]);
-      });
+      const float2 cg = gt[2 * (L - 1 - i)];
+      constexpr int n = REV ? L - 1 - i : i;
+      s0 = fmaf(cg.x, u[n], s0);
+      s1 = fmaf(cg.y, u[n], s1);
     });
   }
-  float s0 = e0[0], s1 = e1[0];
-  static_for<1, S>([&](auto j) {
-    float r0, r1;
-    mv4(t.ps, s0, s1, r0, r1);
-    s0 = r0 + e0[j];
-    s1 = r1 + e1[j];
-  });
   OMEGA_STAMP(SB);
   // 2) inclusive scan of the chunk end states in processing order, S_l += P^d S_{l-d}: within rows
   // of 16 lanes by DPP shifts (d = 1, 2, 4, 8), then row 1 and 3 take row 0 / 2's last prefix and
@@ -204,52 +165,20 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
   const float i0 = vl == 0 ? k0 : p0;
   const float i1 = vl == 0 ? k1 : p1;
   OMEGA_STAMP(SB + 3);
-  // 5) the chunk from its true incoming state: each sub-chunk's incoming state follows from the
-  // previous one's (A^LS in + its zero-state end state), then all run interleaved. (The samples pass
-  // through an opaque copy first (OPQ, the batch kernel): otherwise the compiler keeps step 1's B1 * u
-  // products live across the scan for reuse here -- L more live registers, spilled there; the
-  // standalone kernel runs faster without the copy.)
-  if constexpr (OPQ && !kKwCorr) {
+  // 5) the chunk from its true incoming state. (The samples pass through an opaque copy first (OPQ,
+  // the batch kernel): otherwise the compiler keeps step 1's products' operands live across the scan
+  // for reuse here -- L more live registers, spilled there; the standalone kernel runs faster without
+  // the copy.) (Outputs as zero-state outputs plus a first-row-of-A^i correction -- 7 instead of 9
+  // VALU ops per sample -- spilled the batch kernel: 126 vs 77 us, MI355X round 2; deleted.)
+  if constexpr (OPQ) {
 #pragma unroll
     for (int i = 0; i < L; ++i) asm volatile("" : "+v"(u[i]));
   }
-  if constexpr (kKwCorr) {
-    // y = y_zero + (A^i s_in)[0]: the zero-state outputs plus the first row of A^i (h0, h1) times the
-    // sub-chunk's true incoming state -- independent multiply-adds instead of a second serial pass
-    float r0[S], r1[S];
-    r0[0] = i0;
-    r1[0] = i1;
-    static_for<1, S>([&](auto j) {
-      float q0, q1;
-      mv4(t.ps, r0[j - 1], r1[j - 1], q0, q1);
-      r0[j] = q0 + e0[j - 1];
-      r1[j] = q1 + e1[j - 1];
-    });
-    static_for<0, LS>([&](auto i) {
-      // (groups of 8 rows: the LDS reads are not all hoisted into registers at once)
-      if constexpr (i % 8 == 0) asm volatile("" ::: "memory");
-      const float4 hg = pwl[64 + i];  // (h0, h1) of A^i, LDS broadcast
-      const float g0 = hg.x, g1 = hg.y;
-      static_for<0, S>([&](auto j) {
-        constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
-        u[n] = fmaf(g1, r1[j], fmaf(g0, r0[j], u[n]));
-      });
-    });
-  } else {
-    float r0[S], r1[S];
-    r0[0] = i0;
-    r1[0] = i1;
-    static_for<1, S>([&](auto j) {
-      float q0, q1;
-      mv4(t.ps, r0[j - 1], r1[j - 1], q0, q1);
-      r0[j] = q0 + e0[j - 1];
-      r1[j] = q1 + e1[j - 1];
-    });
-    static_for<0, LS>([&](auto i) {
-      static_for<0, S>([&](auto j) {
-        constexpr int n = REV ? L - 1 - (j * LS + i) : j * LS + i;
-        u[n] = bq_step(t, u[n], r0[j], r1[j]);
-      });
+  {
+    float r0 = i0, r1 = i1;
+    static_for<0, L>([&](auto i) {
+      constexpr int n = REV ? L - 1 - i : i;
+      u[n] = bq_step(t, u[n], r0, r1);
     });
   }
   OMEGA_STAMP(SB + 4);

@@ -28,13 +28,10 @@ OMEGA_STAMPS_DECL
 
 namespace omega {
 
-// OMEGA_KW_WG_PER_CU: workgroups per CU the register budget is sized for (0: compiler's choice); two
-// 512-thread workgroups per CU (128 VGPRs, a few spilled loop invariants) measured 22.3 us vs 25.4 us
-// for one (134 VGPRs) on the cfg2 batch
-#ifndef OMEGA_KW_WG_PER_CU
-#define OMEGA_KW_WG_PER_CU 2
-#endif
-constexpr int kw_waves_per_eu(int nth) { return OMEGA_KW_WG_PER_CU * nth / 256 > 0 ? OMEGA_KW_WG_PER_CU * nth / 256 : 1; }
+// the register budget is sized for two workgroups per CU: two 512-thread workgroups (128 VGPRs, a few
+// spilled loop invariants) measured 22.3 us vs 25.4 us for one (134 VGPRs) on the cfg2 batch
+constexpr int kKwWgPerCu = 2;
+constexpr int kw_waves_per_eu(int nth) { return kKwWgPerCu * nth / 256 > 0 ? kKwWgPerCu * nth / 256 : 1; }
 
 // PUB: the LUFS value is published for a consumer on another stream (KWeightParams::kw_done); a
 // separate instantiation, so the plain kernel keeps its register allocation

@@ -502,10 +502,7 @@ __device__ __forceinline__ void meter_query_body(const MeterPrepParams& p) {
     int jb = 0;
     // kExtRounds rounds of 64 extras loaded together (one L2 latency per group instead of per round:
     // the query runs beside the batch kernel, and its resident time costs the batch register slots)
-#ifndef OMEGA_EXT_ROUNDS
-#define OMEGA_EXT_ROUNDS 4
-#endif
-    constexpr int kExtRounds = OMEGA_EXT_ROUNDS;
+    constexpr int kExtRounds = 4;
     for (int g0 = 0; g0 < ne; g0 += 64 * kExtRounds) {
       MeterExt eg[kExtRounds];
 #pragma unroll

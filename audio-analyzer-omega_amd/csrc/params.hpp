@@ -42,15 +42,10 @@ struct SpectralParams {
   // true peak (professional_meters.py:283-299)
   float* tp_out;      // [n_cf] or nullptr
   const float2* rot;  // [W/2 + 1] exp(+2 pi i k / (4W))
-  float4* tp_scratch;  // [n_cf, W/4] half-spectrum pairs of the 512-thread true-peak kernel (L2-resident)
   // true-peak phases y(n + P/4) computed besides the samples (P = 0): bit P set. 0xE = 4x
   // oversampling (the reference's default), 0x4 = 2x (n + 1/2 only), 0 = 1x (the samples)
   int tp_phases;
   const float2* tw[kMaxLog2];  // tw[l][m] = exp(-2 pi i m / 2^l)
-  // register-FFT inter-pass twiddle tables per size (index 0: K = 4096, 1: K = 8192; null: power
-  // chains): rtw1[j * NTH + t] = (W_K^{t (2j+1)}, W_K^{t (2j+2)}), rtw2[j * L + u] the same for 16 u
-  const float4* rtw1[2];
-  const float4* rtw2[2];
   int rf_sizes;  // host-side launch choice: bit log2(N) set = resolution size N runs on the register-FFT kernel
   // batch_kernel's true-peak role: when set, the value is stored write-through and the workgroup adds 1
   // after it (the true-peak meter query on the side stream waits for the batch's count)
@@ -64,55 +59,16 @@ struct BiquadTab {
   float zi0, zi1;      // scipy.signal.lfilter_zi
   float h0[64], h1[64];  // first row of A^n, n < L (zero-input response of a chunk)
   float pw[64][4];     // P^(l+1), P = A^L, row-major 2x2
-  float psub[4];       // A^(L / kKwSub): the sub-chunk step inside one thread's chunk
   float g0[64], g1[64];  // A^j B, j < L: a sample's share of its (sub-)chunk's zero-state end state
 };
 
-// each thread runs its chunk as kKwSub interleaved sub-chunks (independent recurrences: ILP)
-#ifndef OMEGA_KW_SUB
-#define OMEGA_KW_SUB 1
-#endif
-constexpr int kKwSub = OMEGA_KW_SUB;
-// lfilter_pass: zero-state outputs + first-row-of-A^i correction (1) or a zero-state state pass and a
-// second serial pass from the true incoming state (0, default). The correction form has 7 instead of
-// 9 VALU ops per sample and one serial chain instead of two, but its live ranges cost ~28 VGPRs: the
-// batch kernel spilled (private segment 8 -> 136-444 B) and took 126 vs 77 us (MI355X, round 2).
-#ifndef OMEGA_KW_CORR
-#define OMEGA_KW_CORR 0
-#endif
-constexpr bool kKwCorr = OMEGA_KW_CORR != 0;
-// lfilter_pass step 1 (the zero-state end state of a chunk) as two dot products with the A^j B table
-// (LDS broadcast reads: 2 independent FMAs per sample) instead of the serial state recurrence (4
-// dependent VALU ops per sample).
-#ifndef OMEGA_KW_ZTAB
-#define OMEGA_KW_ZTAB 1
-#endif
-constexpr bool kKwZtab = OMEGA_KW_ZTAB != 0;
 // K-weighting LDS table per filter (float4 entries): [0, 64) the scan powers P^(l+1), [64, 96) the
 // first row of A^i and A^i B, i < 32, as (h0, h1, g0, g1) -- read where used, not held in registers
 constexpr int kPwl = 96;
-// register-FFT inter-pass twiddles from tables (1) or power chains (0, default). The tables cut the
-// FFT roles' VALU count (true peak 2584 -> 2396 static instructions) but ran slower on MI355X (round 2:
-// true peak 37.5 vs 36.4 us, batch 79.5 vs 78.1, cfg3 67.1 vs 65.6): these kernels are bound by LDS
-// exchanges and barriers, not VALU issue, and the table loads add latency.
-#ifndef OMEGA_RF_TWTAB
-#define OMEGA_RF_TWTAB 0
-#endif
-constexpr bool kRfTab = OMEGA_RF_TWTAB != 0;
-// true peak: lane l and lane l ^ 63 of a wave own mirror spectrum columns (t, NTH - t), so each phase's
-// mirror spectrum comes by ds_bpermute inside the wave (1) instead of an LDS exchange with two
-// workgroup barriers (0)
-#ifndef OMEGA_TP_PAIR
-#define OMEGA_TP_PAIR 1
-#endif
-constexpr bool kTpPair = OMEGA_TP_PAIR != 0;
-
 // K-weighting workgroup: up to 32 samples per thread (M/32 threads, 64..512), the chunk length L of
 // the scan tables (make_biquad_tab) follows from it.
 constexpr int kw_threads(int M) { return M / 32 < 64 ? 64 : (M / 32 > 512 ? 512 : M / 32); }
 constexpr int kw_chunk(int M) { return M / kw_threads(M); }
-// the fused frame kernel (frame.hip) runs K-weighting for 16384-sample frames at 1024 threads
-constexpr int kFrameChunk = 16;
 
 struct KWeightParams {
   const float* x;
@@ -250,39 +206,12 @@ struct MultiPlan {
 //       the roles of a frame land on one XCD (blockIdx % 8) and a CU sees the roles mixed
 //   [seg_begin[2], ...)  the resolutions of at most 8192 points (multi; wg_begin relative to seg_begin[2])
 // The K-weighting role counts itself into KWeightParams::kw_done when that is set.
-// the rejected meter-scheduling experiments inside batch_kernel (the join, the true-peak meter role:
-// capi.cpp omega_ctx::batch_join / tp_meter_in_batch) are compiled in only with OMEGA_BATCH_EXTRAS=1,
-// so that the product kernel carries neither their branches nor their kernel-argument bytes
-#ifndef OMEGA_BATCH_EXTRAS
-#define OMEGA_BATCH_EXTRAS 0
-#endif
-constexpr bool kBatchExtras = OMEGA_BATCH_EXTRAS != 0;
-
 struct BatchPlan {
   int seg_begin[3];
   int n_roles[2];
   int roles[2][3];
   int mr_res;
   MultiPlan multi;
-#if OMEGA_BATCH_EXTRAS
-  // the join (omega_ctx::batch_join): every workgroup counts itself into wg_done when it is finished;
-  // the one that completes the count (wg_target) does not finish before (int)(*join_ctr - join_target)
-  // >= 0 (the side stream's meter queries), bounded by poll_limit, expiry -> err_word[1]
-  unsigned* wg_done;
-  unsigned wg_target;
-  unsigned* join_ctr;
-  unsigned join_target;
-  int poll_limit;
-  unsigned* err_word;
-  // the true-peak meter as the grid's last workgroup (omega_ctx::tp_meter_in_batch, one meter chunk):
-  // workgroup tpm_wg (-1: none) waits (bounded) for the batch's true-peak count (SpectralParams::
-  // tp_done >= tp_target) and for the side stream's LUFS-query count (join_ctr >= join_target), then
-  // computes column 4 of the meters and rolls the true-peak history of mq, as meter_query_kernel's
-  // true-peak part would after the batch
-  int tpm_wg;
-  unsigned tp_target;
-  MeterPrepParams mq;
-#endif
 };
 
 // Fused spectrum analysis (cfg3): windowed rfft magnitude (A13) -> log-band max (A10) and raw
@@ -308,8 +237,6 @@ struct SpectraParams {
   // the same weights permuted into group order as 32-byte records {w0, w1, w2, w3 | w4, bin, -, -}
   // (the register-FFT kernel reads record j directly: no dependent permutation load)
   const float4* crec;      // [2 * cgoff[12]]
-  const float4* rtw1;      // register-FFT twiddle tables for K = 4096 (SpectralParams::rtw1)
-  const float4* rtw2;
   double* chroma_out;      // [n, 12] or nullptr (smoothed, normalised; before the temporal blend)
   const float2* tw[kMaxLog2];
 };

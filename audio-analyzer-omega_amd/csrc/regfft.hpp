@@ -39,16 +39,9 @@ __device__ __forceinline__ float lane_xor1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
 
-// TIGHT (K = 4096 only): the exchanges in exactly K slots (32 KiB, no padding) -- XOR swizzles
-// instead of padded rows, conflict-free as the padded layout (tools/model/regfft_model.py --tight):
-//   exchange 1  (t, k1)      -> 256 k1 + (t ^ 16 (k1 & 1))
-//   exchange 2  (u, k2, k1)  -> 256 k1 + 16 (k2 ^ (k1 & 1)) + (u ^ k2)   (per-access XOR addresses)
-//   spectrum    n            -> n ^ ((n >> 4) & 15)
-// so that a 256-thread workgroup's whole LDS fits 32 KiB (five per CU instead of four).
-template <int K, bool TIGHT = false>
+template <int K>
 struct RegFFT {
   static_assert(K == 8192 || K == 4096, "register FFT plans: K = 4096, 8192");
-  static_assert(!TIGHT || K == 4096, "the tight layout is for K = 4096");
   static constexpr int NTH = K / 16;
   static constexpr int L = K / 256;
   // LDS layouts (float2 slots), padded so that every slot is a per-thread base plus a compile-time
@@ -59,21 +52,22 @@ struct RegFFT {
   static constexpr int P1 = L == 32 ? 512 : 272;
   static constexpr int P2R = L == 32 ? 544 : 272;
   static constexpr int P2C = L == 32 ? 34 : 17;
-  static constexpr int kSlots = TIGHT ? 4096 : (K == 8192 ? 8712 : 4352);  // LDS buffer size in float2
+  static constexpr int kSlots = K == 8192 ? 8712 : 4352;  // LDS buffer size in float2
+  // pass-2 twiddle table in LDS: t2[(k2 - 1) L + u] = W_K^{16 u k2}, k2 = 1..15, u < L (3.75 KiB for
+  // K = 8192): 15 broadcast-free ds_read_b64 per pass instead of the 14-multiplication power chain
+  static constexpr int kT2 = 15 * L;
 
   static __device__ __forceinline__ int a3(int n) {
-    if constexpr (TIGHT) return n ^ ((n >> 4) & 15);
-    else if constexpr (K == 8192) return n + (n >> 4) + ((n >> 12) << 3);
+    if constexpr (K == 8192) return n + (n >> 4) + ((n >> 12) << 3);
     else return n + (n >> 4);
   }
   // bins k = t + NTH r: a3(k) = s3(t) + o3(r)
   static __device__ __forceinline__ int s3(int t) {
-    if constexpr (TIGHT) return t ^ ((t >> 4) & 15);
-    else return t + (t >> 4);
+    return t + (t >> 4);
   }
-  static constexpr int o3(int r) { return TIGHT ? 256 * r : (K == 8192 ? 544 * r + 8 * (r >> 3) : 272 * r); }
+  static constexpr int o3(int r) { return K == 8192 ? 544 * r + 8 * (r >> 3) : 272 * r; }
   // mirror bins K - t - NTH r, t >= 1: s3m(t) + o3(15 - r) (t = 0: exact except r = 0 (slot K: the
-  // callers' slack, or a guarded read under TIGHT) and, for K = 8192, r = 8)
+  // callers' slack) and, for K = 8192, r = 8)
   static __device__ __forceinline__ int s3m(int t) { return s3(NTH - t); }
   // pass-3 output register m of thread s: frequency out_index(s, m), slot s3o(s) + 272 m
   static __device__ __forceinline__ int out_index(int s, int m) {
@@ -81,11 +75,10 @@ struct RegFFT {
     else return (s >> 4) + 16 * (s & 15) + 256 * m;
   }
   static __device__ __forceinline__ int s3o(int s) {
-    if constexpr (TIGHT) return ((s >> 4) ^ (s & 15)) + 16 * (s & 15);
-    else if constexpr (L == 32) return (s >> 5) + 17 * ((s >> 1) & 15) + 4360 * (s & 1);
+    if constexpr (L == 32) return (s >> 5) + 17 * ((s >> 1) & 15) + 4360 * (s & 1);
     else return (s >> 4) + 17 * (s & 15);
   }
-  static constexpr int o3o(int m) { return TIGHT ? 256 * m : 272 * m; }
+  static constexpr int o3o(int m) { return 272 * m; }
 
   // v[k] *= w^k, k = 1..15 (powers by a multiply chain)
   static __device__ __forceinline__ void twiddle(float2 (&v)[16], float2 w) {
@@ -104,52 +97,40 @@ struct RegFFT {
     static_for<0, 16>([&](auto m) { v[m] = o[m]; });
   }
 
-  // v[k] *= T[k], k = 1..15, from a twiddle table: tab[j * stride] = (T[2j + 1], T[2j + 2]), j < 8
-  static __device__ __forceinline__ void twiddle_tab(float2 (&v)[16], const float4 (&q)[8]) {
-    static_for<0, 8>([&](auto j) {
-      v[2 * j + 1] = cmul(v[2 * j + 1], make_float2(q[j].x, q[j].y));
-      if constexpr (2 * j + 2 < 16) v[2 * j + 2] = cmul(v[2 * j + 2], make_float2(q[j].z, q[j].w));
-    });
+  // fill the pass-2 table (every thread of the workgroup; published by the first exchange's barrier)
+  static __device__ __forceinline__ void fill_t2(float2* t2, const float2* __restrict__ twK, int tid) {
+    for (int i = tid; i < kT2; i += NTH) {
+      const int k2 = i / L + 1, u = i % L;
+      t2[i] = twK[(16 * u * k2) & (K - 1)];
+    }
   }
-  static __device__ __forceinline__ void load_tab(float4 (&q)[8], const float4* __restrict__ tab, int stride) {
-    static_for<0, 8>([&](auto j) { q[j] = tab[j * stride]; });
+  // v[k2] *= W_K^{16 u k2}, k2 = 1..15, from the LDS table (t2u = t2 + u): lanes of one ds_read_b64
+  // group read consecutive entries (u = t % L), conflict-free
+  static __device__ __forceinline__ void twiddle_t2(float2 (&v)[16], const float2* t2u) {
+    static_for<1, 16>([&](auto k2) { v[k2] = cmul(v[k2], t2u[(k2 - 1) * L]); });
   }
 
   // Forward FFT. In: v[r] = x[t + NTH r]. Out: v[m] = X[out_index(t, m)]. w1 = W_K^t and
   // w2 = W_K^{16 (t mod L)} (the thread's twiddle bases, loaded once per kernel). SYNC: `buf` may
   // still be read by other threads on entry -- a barrier precedes the first exchange write (after
-  // pass 1's arithmetic, so the butterflies overlap the stragglers' reads). tw1 / tw2 (optional):
-  // the inter-pass twiddles as tables (RfTw), loaded ahead of each pass's DFT instead of formed by
-  // power chains (14 complex multiplications per pass).
-  template <bool SYNC = false, bool TAB = false>
+  // pass 1's arithmetic, so the butterflies overlap the stragglers' reads). LT2: pass 2's twiddles
+  // from the LDS table t2 (fill_t2; w2 unused) instead of the power chain.
+  template <bool SYNC = false, bool LT2 = false>
   static __device__ __forceinline__ void run(float2 (&v)[16], float2* buf, int t, float2 w1, float2 w2,
-                                             const float4* __restrict__ tw1 = nullptr,
-                                             const float4* __restrict__ tw2 = nullptr) {
-    run2<SYNC, TAB>(v, buf, t, t, w1, w2, tw1, tw2);
+                                             const float2* t2 = nullptr) {
+    run2<SYNC, LT2>(v, buf, t, t, w1, w2, t2);
   }
   // run() with the pass-1 input column t1 (v[r] = x[t1 + NTH r], w1 = W_K^t1) decoupled from the
   // thread's pass-2/3 role t (w2 = W_K^{16 (t mod L)}): any bijection tid -> t1 (the true peak pairs
   // mirror columns t1, NTH - t1 inside one wave).
-  template <bool SYNC = false, bool TAB = false>
+  template <bool SYNC = false, bool LT2 = false>
   static __device__ __forceinline__ void run2(float2 (&v)[16], float2* buf, int t1, int t, float2 w1, float2 w2,
-                                              const float4* __restrict__ tw1 = nullptr,
-                                              const float4* __restrict__ tw2 = nullptr) {
+                                              const float2* t2 = nullptr) {
     // pass 1
-    if constexpr (TAB) {
-      float4 q[8];
-      load_tab(q, tw1 + t1, NTH);
-      dft16(v);
-      twiddle_tab(v, q);
-    } else {
-      dft16(v);
-      twiddle(v, w1);
-    }
+    dft16(v);
+    twiddle(v, w1);
     if constexpr (SYNC) __syncthreads();
-    if constexpr (TIGHT) {
-      float2* b0 = buf + t1;
-      float2* b1 = buf + (t1 ^ 16);
-      static_for<0, 16>([&](auto k1) { (k1 & 1 ? b1 : b0)[256 * k1] = v[k1]; });
-    } else {
+    {
       float2* b = buf + t1;
       static_for<0, 16>([&](auto k1) { b[P1 * k1] = v[k1]; });
     }
@@ -157,46 +138,23 @@ struct RegFFT {
     // pass 2
     {
       const int u = t % L, k1 = t / L;
-      if constexpr (TIGHT) {  // element (u + 16 r, k1) at 256 k1 + u + 16 (r ^ (k1 & 1))
-        const int par = k1 & 1;
-        const float2* be = buf + 256 * k1 + u + 16 * par;
-        const float2* bo = buf + 256 * k1 + u - 16 * par;
-        static_for<0, 16>([&](auto r) { v[r] = (r & 1 ? bo : be)[16 * r]; });
-      } else {
-        const float2* b = buf + P1 * k1 + u;
-        static_for<0, 16>([&](auto r) { v[r] = b[L * r]; });
-      }
-      if constexpr (TAB) {
-        float4 q[8];
-        load_tab(q, tw2 + u, L);
-        dft16(v);
-        twiddle_tab(v, q);
-      } else {
-        dft16(v);
+      const float2* b = buf + P1 * k1 + u;
+      static_for<0, 16>([&](auto r) { v[r] = b[L * r]; });
+      dft16(v);
+      if constexpr (LT2)
+        twiddle_t2(v, t2 + u);
+      else
         twiddle(v, w2);
-      }
       __syncthreads();  // every exchange-1 read is done
-      if constexpr (TIGHT) {  // (u, k2, k1) at 256 k1 + 16 (k2 ^ par) + (u ^ k2)
-        const int par = k1 & 1;
-        float2* be = buf + 256 * k1 + 16 * par;
-        float2* bo = buf + 256 * k1 - 16 * par;
-        static_for<0, 16>([&](auto k2) { (k2 & 1 ? bo : be)[16 * k2 + (u ^ k2)] = v[k2]; });
-      } else {
-        float2* bw = buf + P2R * k1 + u;
-        static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
-      }
+      float2* bw = buf + P2R * k1 + u;
+      static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
     }
     __syncthreads();
     // pass 3
     if constexpr (L == 16) {
       const int k2 = t & 15, k1 = t >> 4;
-      if constexpr (TIGHT) {
-        const float2* b = buf + 256 * k1 + 16 * (k2 ^ (k1 & 1));
-        static_for<0, 16>([&](auto r) { v[r] = b[r ^ k2]; });
-      } else {
-        const float2* b = buf + P2R * k1 + P2C * k2;
-        static_for<0, 16>([&](auto r) { v[r] = b[r]; });
-      }
+      const float2* b = buf + P2R * k1 + P2C * k2;
+      static_for<0, 16>([&](auto r) { v[r] = b[r]; });
       dft16(v);
     } else {
       const int q = t & 1, k2 = (t >> 1) & 15, k1 = t >> 5;
@@ -211,87 +169,6 @@ struct RegFFT {
         v[m] = make_float2(fmaf(v[m].x, s, px), fmaf(v[m].y, s, py));
       });
     }
-  }
-
-  // The pass bodies of run2() as separate steps, for run_pair().
-  static __device__ __forceinline__ void pass1(float2 (&v)[16], float2 w1) {
-    dft16(v);
-    twiddle(v, w1);
-  }
-  static __device__ __forceinline__ void write1(const float2 (&v)[16], float2* buf, int t1) {
-    float2* b = buf + t1;
-    static_for<0, 16>([&](auto k1) { b[P1 * k1] = v[k1]; });
-  }
-  static __device__ __forceinline__ void read1(float2 (&v)[16], const float2* buf, int t) {
-    const int u = t % L, k1 = t / L;
-    const float2* b = buf + P1 * k1 + u;
-    static_for<0, 16>([&](auto r) { v[r] = b[L * r]; });
-  }
-  static __device__ __forceinline__ void pass2(float2 (&v)[16], float2 w2) {
-    dft16(v);
-    twiddle(v, w2);
-  }
-  static __device__ __forceinline__ void write2(const float2 (&v)[16], float2* buf, int t) {
-    const int u = t % L, k1 = t / L;
-    float2* bw = buf + P2R * k1 + u;
-    static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
-  }
-  static __device__ __forceinline__ void read2(float2 (&v)[16], const float2* buf, int t) {
-    if constexpr (L == 16) {
-      const int k2 = t & 15, k1 = t >> 4;
-      const float2* b = buf + P2R * k1 + P2C * k2;
-      static_for<0, 16>([&](auto r) { v[r] = b[r]; });
-    } else {
-      const int q = t & 1, k2 = (t >> 1) & 15, k1 = t >> 5;
-      const float2* b = buf + P2R * k1 + P2C * k2 + q;
-      static_for<0, 16>([&](auto r) { v[r] = b[2 * r]; });
-    }
-  }
-  static __device__ __forceinline__ void pass3(float2 (&v)[16], int t) {
-    dft16(v);
-    if constexpr (L == 32) {
-      const int q = t & 1;
-      if (q) static_for<1, 16>([&](auto m) { v[m] = twc<m, 32>(v[m]); });
-      const float s = q ? -1.f : 1.f;
-      static_for<0, 16>([&](auto m) {
-        const float px = lane_xor1(v[m].x), py = lane_xor1(v[m].y);
-        v[m] = make_float2(fmaf(v[m].x, s, px), fmaf(v[m].y, s, py));
-      });
-    }
-  }
-
-  // Two frames' forward FFTs (a, b: same plan, same thread roles as run2()) through ONE exchange
-  // buffer, interleaved so that each frame's butterflies fill the other frame's LDS exchange: while
-  // the buffer carries frame a, the waves compute frame b and the other way round. Every buffer use is
-  // write -> barrier -> read -> barrier (the reads done before the other frame writes); the other
-  // frame's pass sits between a write and its barrier (the wave's stores drain and the slower waves
-  // catch up meanwhile). Two frames in flight per workgroup on one 64 KiB buffer: a CU holds four
-  // frames instead of two. SYNC: a barrier before the first write (the buffer may still be read).
-  template <bool SYNC = false>
-  static __device__ __forceinline__ void run_pair(float2 (&a)[16], float2 (&b)[16], float2* buf, int t1, int t,
-                                                  float2 w1, float2 w2) {
-    pass1(a, w1);
-    if constexpr (SYNC) __syncthreads();
-    write1(a, buf, t1);
-    pass1(b, w1);
-    __syncthreads();
-    read1(a, buf, t);
-    __syncthreads();
-    write1(b, buf, t1);
-    pass2(a, w2);
-    __syncthreads();
-    read1(b, buf, t);
-    __syncthreads();
-    write2(a, buf, t);
-    pass2(b, w2);
-    __syncthreads();
-    read2(a, buf, t);
-    __syncthreads();
-    write2(b, buf, t);
-    pass3(a, t);
-    __syncthreads();
-    read2(b, buf, t);
-    pass3(b, t);
   }
 
   // Natural-order spectrum exchange after run(): every register to its frequency's slot

@@ -30,16 +30,21 @@ OMEGA_WGTRACE_DECL
 
 namespace omega {
 
-// LDS of one workgroup: the padded exchange buffer, 8 slots of slack for the t = 0 mirror reads, and
-// the block-reduction scratch
+// LDS of one workgroup: the padded exchange buffer, 8 slots of slack for the t = 0 mirror reads, the
+// block-reduction scratch and the pass-2 twiddle table (RegFFT::fill_t2)
 template <int K>
-constexpr size_t lds_bytes() { return (RegFFT<K>::kSlots + 8) * sizeof(float2) + 64; }
+constexpr size_t t2_offset() { return (RegFFT<K>::kSlots + 8) * sizeof(float2) + 64; }
+template <int K>
+constexpr size_t lds_bytes() { return t2_offset<K>() + RegFFT<K>::kT2 * sizeof(float2); }
+template <int K>
+__device__ __forceinline__ float2* t2_table(char* smem) { return reinterpret_cast<float2*>(smem + t2_offset<K>()); }
 
-// kTpPair column map: thread tid = 64 w + l owns spectrum column t = 32 w + l (l < 32), and lane
-// l ^ 63 the mirror column NTH - t (column NTH / 2 for t = 0); columns 0 and NTH / 2 mirror themselves
+// Column map of the true peak: thread tid = 64 w + l owns spectrum column t = 32 w + l (l < 32), and
+// lane l ^ 63 the mirror column NTH - t (column NTH / 2 for t = 0); columns 0 and NTH / 2 mirror
+// themselves -- each phase's mirror spectrum comes by ds_bpermute inside the wave instead of an LDS
+// exchange with two barriers
 template <int NTH>
 __device__ __forceinline__ int tp_column(int tid) {
-  if constexpr (!kTpPair) return tid;
   const int w = tid >> 6, l = tid & 63;
   if (l < 32) return 32 * w + l;
   const int a = 32 * w + (63 - l);
@@ -65,15 +70,15 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
   const float2 w1 = twK[t], w2 = twK[16 * (tid % FFT::L)];
   const float2 wm = twM[t];     // W_M^t
   const float2 rho = p.rot[t];  // e^{2 pi i t / 4M}
+  float2* t2 = t2_table<K>(smem);
+  FFT::fill_t2(t2, twK, tid);
   asm volatile("" ::: "memory");  // (keeps the scheduler from sinking them behind the frame loads)
   static_for<0, 16>([&](auto r) {
     v[r] = x2[t + NTH * r];
     mx = fmaxf(mx, fmaxf(fabsf(v[r].x), fabsf(v[r].y)));
   });
   OMEGA_STAMP(1);
-  const float4* __restrict__ rt1 = p.rtw1[K == 8192];
-  const float4* __restrict__ rt2 = p.rtw2[K == 8192];
-  FFT::template run2<false, kRfTab>(v, buf, t, tid, w1, w2, rt1, rt2);
+  FFT::template run2<false, true>(v, buf, t, tid, w1, w2, t2);
   OMEGA_STAMP(2);
   // natural-order spectrum -> X_k on k in S_t
   __syncthreads();
@@ -106,7 +111,7 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
   // i e^{2 pi i t / M} / 2: alpha_k = (1/2, 0) + (that) e^{2 pi i r / 32}
   const float2 hz = make_float2(0.5f * wm.y, 0.5f * wm.x);
   float fmx = 0.f;
-  // kTpPair: byte address of the lane holding the mirror column (itself for columns 0 and NTH / 2)
+  // byte address of the lane holding the mirror column (itself for columns 0 and NTH / 2)
   const int lane = tid & 63;
   const int mir_addr = 4 * ((t == 0 || t == NTH / 2) ? lane : lane ^ 63);
   OMEGA_STAMP(4);
@@ -125,35 +130,17 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
     if (!((p.tp_phases >> P) & 1)) continue;  // phase not requested (oversampling 2 or 1)
     OMEGA_STAMP(1 + 4 * P);
     const float cp = P == 1 ? 7.071067812e-01f : (P == 2 ? 0.f : -7.071067812e-01f);
-    const float2* bm = buf + FFT::s3m(tl);
-    if constexpr (!kTpPair) {
-      __syncthreads();  // the previous transform's last exchange reads are done
-      float2* bo = buf + FFT::s3(tl);
-      static_for<0, 16>([&](auto r) { bo[FFT::o3(r)] = y[r]; });
-      __syncthreads();
-    }
     OMEGA_STAMP(2 + 4 * P);
     static_for<0, 16>([&](auto r) {
-      float2 yp;
-      if constexpr (kTpPair) {
-        // Y_{K-k}, k = t + NTH r: register 15 - r of the mirror lane (t >= 1); column 0 holds its own
-        // mirrors in register 16 - r (r >= 1)
-        const float2 m = y[15 - r];
-        yp = make_float2(__int_as_float(__builtin_amdgcn_ds_bpermute(mir_addr, __float_as_int(m.x))),
-                         -__int_as_float(__builtin_amdgcn_ds_bpermute(mir_addr, __float_as_int(m.y))));
-        if constexpr (r == 0) {
-          if (tl == 0) yp = make_float2(xn * cp, 0.f);
-        } else {
-          if (tl == 0) yp = cconj(y[16 - r]);
-        }
+      // Y_{K-k}, k = t + NTH r: register 15 - r of the mirror lane (t >= 1); column 0 holds its own
+      // mirrors in register 16 - r (r >= 1)
+      const float2 m = y[15 - r];
+      float2 yp = make_float2(__int_as_float(__builtin_amdgcn_ds_bpermute(mir_addr, __float_as_int(m.x))),
+                              -__int_as_float(__builtin_amdgcn_ds_bpermute(mir_addr, __float_as_int(m.y))));
+      if constexpr (r == 0) {
+        if (tl == 0) yp = make_float2(xn * cp, 0.f);
       } else {
-        yp = cconj(bm[FFT::o3(15 - r)]);
-        if constexpr (r == 0) {
-          if (tl == 0) yp = make_float2(xn * cp, 0.f);
-        }
-        if constexpr (K == 8192 && r == 8) {
-          if (tl == 0) yp = cconj(y[8]);
-        }
+        if (tl == 0) yp = cconj(y[16 - r]);
       }
       const float2 g = twc<-r, 32>(hzl);  // (i e_t / 2) e^{2 pi i r / 32}
       const float2 al = make_float2(0.5f + g.x, g.y);
@@ -161,7 +148,7 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
       v[r] = cconj(cadd(yp, cmul(al, d)));
     });
     OMEGA_STAMP(3 + 4 * P);
-    FFT::template run2<true, kRfTab>(v, buf, tl, tidl, w1l, w2l, rt1, rt2);
+    FFT::template run2<true, true>(v, buf, tl, tidl, w1l, w2l, t2);
     static_for<0, 16>([&](auto m) { fmx = fmaxf(fmx, fmaxf(fabsf(v[m].x), fabsf(v[m].y))); });
     OMEGA_STAMP(4 + 4 * P);
   }
@@ -182,13 +169,6 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
 template <int K>
 __global__ __launch_bounds__(K / 16, 4) void truepeak_rf_kernel(SpectralParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-#ifdef OMEGA_TP_STAGGER
-  // development experiment: the second half of the grid (the workgroups that share a CU with the
-  // first half's) starts later, so the two do not run the same phase at the same time
-  if (blockIdx.x >= gridDim.x / 2) {
-    for (int i = 0; i < OMEGA_TP_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-#endif
   OMEGA_WG_BEGIN();
   truepeak_rf_body<K>(p, blockIdx.x, threadIdx.x, smem);
   OMEGA_WG_END(1);
@@ -212,6 +192,8 @@ __device__ __forceinline__ void mrfft_rf_body(const SpectralParams& p, int r, in
   float2 v[16];
   const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];  // (issued before the frame: see truepeak_rf_body)
   const float2 wm = twM[t];
+  float2* t2 = t2_table<K>(smem);
+  FFT::fill_t2(t2, twK, t);
   asm volatile("" ::: "memory");
   static_for<0, 16>([&](auto q) {
     const float2 a = x2[t + NTH * q], w = w2[t + NTH * q];
@@ -221,7 +203,7 @@ __device__ __forceinline__ void mrfft_rf_body(const SpectralParams& p, int r, in
   const int e0 = rp.ent_begin + t;
   CombEnt ent{};
   if (p.comb_out && e0 < rp.ent_end) ent = p.ent[e0];
-  FFT::template run<false, kRfTab>(v, buf, t, w1, w2b, p.rtw1[K == 8192], p.rtw2[K == 8192]);
+  FFT::template run<false, true>(v, buf, t, w1, w2b, t2);
   __syncthreads();
   FFT::store_spectrum(v, buf, t);
   __syncthreads();
@@ -274,116 +256,6 @@ __device__ __forceinline__ void mrfft_rf_body(const SpectralParams& p, int r, in
   for (int e = e0 + NTH; e < rp.ent_end; e += NTH) apply(p.ent[e]);
 }
 
-// Two frames (cfa, cfb) of one resolution through one workgroup and one exchange buffer
-// (RegFFT::run_pair): the same outputs as mrfft_rf_body on each. has_b false: the second slot repeats
-// frame a and stores nothing.
-template <int K>
-__device__ __forceinline__ void mrfft_rf_pair_body(const SpectralParams& p, int r, int64_t cfa, int64_t cfb, bool has_b,
-                                                   int t, char* smem) {
-  using FFT = RegFFT<K>;
-  constexpr int NTH = FFT::NTH;
-  float2* buf = reinterpret_cast<float2*>(smem);
-  const ResParam& rp = p.res[r];
-  auto frame = [&](int64_t cf) {
-    const int64_t f = cf / p.C, c = cf % p.C;
-    return reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride + rp.offset);
-  };
-  const float2* xa = frame(cfa);
-  const float2* xb = frame(has_b ? cfb : cfa);
-  const float2* w2 = reinterpret_cast<const float2*>(rp.win);
-  const float2* __restrict__ twK = p.tw[ilog2(K)];
-  const float2* __restrict__ twM = p.tw[ilog2(2 * K)];
-  float2 a[16], b[16];
-  const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];
-  const float2 wm = twM[t];
-  asm volatile("" ::: "memory");
-  static_for<0, 16>([&](auto q) {
-    const float2 u = xa[t + NTH * q], v = xb[t + NTH * q], w = w2[t + NTH * q];
-    a[q] = make_float2(u.x * w.x, u.y * w.y);
-    b[q] = make_float2(v.x * w.x, v.y * w.y);
-  });
-  FFT::template run_pair<false>(a, b, buf, t, t, w1, w2b);
-  // natural-order spectra one frame at a time through the buffer; |X_k| on the thread's bins
-  float mga[16], mgb[16];
-  float nya = 0.f, nyb = 0.f;
-  auto untangle_mag = [&](const float2 (&v)[16], float (&mg)[16], float& mnyq) {
-    __syncthreads();
-    FFT::store_spectrum(v, buf, t);
-    __syncthreads();
-    const float2* bo = buf + FFT::s3(t);
-    const float2* bm = buf + FFT::s3m(t);
-    static_for<0, 16>([&](auto q) {
-      const float2 x0 = bo[FFT::o3(q)];
-      float2 x1 = bm[FFT::o3(15 - q)];
-      if constexpr (K == 8192 && q == 8) {
-        if (t == 0) x1 = x0;
-      }
-      float2 xk, xkk;
-      untangle(x0, x1, twc<q, 32>(wm), xk, xkk);
-      mg[q] = cabs(xk);
-      if constexpr (q == 0) {
-        if (t == 0) {
-          mg[0] = fabsf(x0.x + x0.y);
-          mnyq = fabsf(x0.x - x0.y);
-        }
-      }
-    });
-  };
-  untangle_mag(a, mga, nya);
-  untangle_mag(b, mgb, nyb);
-  if (rp.mag_out) {
-    const float* __restrict__ wgt = rp.wgt;
-    float* oa = rp.mag_out + cfa * (K + 1);
-    static_for<0, 16>([&](auto q) { oa[t + NTH * q] = mga[q] * wgt[t + NTH * q]; });
-    if (t == 0) oa[K] = nya * wgt[K];
-    if (has_b) {
-      float* ob = rp.mag_out + cfb * (K + 1);
-      static_for<0, 16>([&](auto q) { ob[t + NTH * q] = mgb[q] * wgt[t + NTH * q]; });
-      if (t == 0) ob[K] = nyb * wgt[K];
-    }
-  }
-  if (!p.comb_out) return;
-  // both frames' magnitudes parked side by side (2 (K + 1) floats fit the exchange buffer)
-  float* mag = reinterpret_cast<float*>(smem);
-  __syncthreads();
-  static_for<0, 16>([&](auto q) {
-    mag[t + NTH * q] = mga[q];
-    mag[K + 1 + t + NTH * q] = mgb[q];
-  });
-  if (t == 0) {
-    mag[K] = nya;
-    mag[2 * K + 1] = nyb;
-  }
-  __syncthreads();
-  float* oa = p.comb_out + cfa * p.T;
-  float* ob = p.comb_out + cfb * p.T;
-  auto apply = [&](const CombEnt& en) {
-    const int tt = en.tm & 0xFFFFFF, op = en.tm >> 24;
-    const float va = fmaf(en.c1, mag[en.j + 1], en.c0 * mag[en.j]);
-    const float vb = fmaf(en.c1, mag[K + 1 + en.j + 1], en.c0 * mag[K + 1 + en.j]);
-    if (op == 0) {
-      oa[tt] = va;
-      if (has_b) ob[tt] = vb;
-    } else if (op == 1) {
-      oa[tt] += va;
-      if (has_b) ob[tt] += vb;
-    } else {
-      oa[tt] = 0.f;
-      if (has_b) ob[tt] = 0.f;
-    }
-  };
-  for (int e = rp.ent_begin + t; e < rp.ent_end; e += NTH) apply(p.ent[e]);
-}
-
-template <int K>
-__global__ __launch_bounds__(K / 16, 4) void mrfft_rf_pair_kernel(SpectralParams p, int r) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int64_t cfa = 2 * (int64_t)blockIdx.x, cfb = cfa + 1;
-  OMEGA_WG_BEGIN();
-  mrfft_rf_pair_body<K>(p, r, cfa, cfb, cfb < p.n_cf, threadIdx.x, smem);
-  OMEGA_WG_END(12);
-}
-
 template <int K>
 __global__ __launch_bounds__(K / 16, 4) void mrfft_rf_kernel(SpectralParams p, int r) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -394,11 +266,6 @@ __global__ __launch_bounds__(K / 16, 4) void mrfft_rf_kernel(SpectralParams p, i
 
 OMEGA_STAMPS_GETTER(omega_debug_rf_stamps)
 OMEGA_WGTRACE_GETTER(omega_debug_wgtrace)
-
-hipError_t launch_mrfft_rf_pair(const SpectralParams& p, int r, hipStream_t s) {
-  hipLaunchKernelGGL(mrfft_rf_pair_kernel<8192>, dim3((unsigned)((p.n_cf + 1) / 2)), dim3(512), lds_bytes<8192>(), s, p, r);
-  return hipGetLastError();
-}
 
 hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
@@ -418,23 +285,11 @@ hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s)
 // band and chroma tables are read from global memory, L1/L2-resident).
 constexpr int kSpecRfThreads = 256;
 constexpr int kSpecRfPeakWords = 12;  // peaks among bins < 64 * 12 = 768: suppression reaches k / 2 < 1536 / 2
-// OMEGA_SPEC_PREFETCH: the band-table entries and the first chroma records loaded ahead of the
-// transform (1) or where they are used (0)
-#ifndef OMEGA_SPEC_PREFETCH
-#define OMEGA_SPEC_PREFETCH 1
-#endif
-constexpr bool kSpecPrefetch = OMEGA_SPEC_PREFETCH != 0;
-// OMEGA_SPEC_TIGHT: the cfg3 kernel's transform on the 32 KiB tight layout (RegFFT<4096, true>: five
-// workgroups per CU) or on the padded one (34.9 KiB: four)
-#ifndef OMEGA_SPEC_TIGHT
-#define OMEGA_SPEC_TIGHT 0
-#endif
-constexpr bool kSpecTight = OMEGA_SPEC_TIGHT != 0;
 
 
 template <int K>
 __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraParams p) {
-  using FFT = RegFFT<K, kSpecTight>;
+  using FFT = RegFFT<K>;
   constexpr int NTH = FFT::NTH;
   static_assert(NTH == kSpecRfThreads, "one 256-thread workgroup per frame");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -462,6 +317,9 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   const float2* __restrict__ twK = p.tw[ilog2(K)];
   const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];  // (issued before the frame: see truepeak_rf_body)
   const float2 wm = p.tw[ilog2(2 * K)][t];
+  // pass-2 twiddle table after the exchange buffer and its slack (RegFFT::fill_t2)
+  float2* t2 = reinterpret_cast<float2*>(smem + (FFT::kSlots + 8) * sizeof(float2));
+  FFT::fill_t2(t2, twK, t);
   // this thread's band-table entries (bands t, t + NTH) and chroma-group bounds, issued with the
   // twiddles ahead of the frame: their latency is off the band / chroma phases' critical path
   constexpr int kGrp = 20;  // chroma: threads per base-class group (12 x 20 = 240 of 256)
@@ -469,14 +327,14 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   float bsc[2] = {1.f, 1.f};
   static_for<0, 2>([&](auto j) {
     const int i = t + NTH * j;
-    if (kSpecPrefetch && p.bands_out && i < p.n_valid) {
+    if (p.bands_out && i < p.n_valid) {
       bs[j] = p.starts[i];
       be[j] = p.ends[i];
       if (p.scale) bsc[j] = p.scale[i];
     }
   });
   int cj0 = 0, cj1 = 0;
-  if (kSpecPrefetch && p.chroma_out && t < 12 * kGrp) {
+  if (p.chroma_out && t < 12 * kGrp) {
     cj0 = p.cgoff[t / kGrp];
     cj1 = p.cgoff[t / kGrp + 1];
   }
@@ -488,7 +346,7 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
     v[r] = make_float2(a.x * w.x, a.y * w.y);
   });
   OMEGA_STAMP(1);
-  FFT::template run<false, kRfTab>(v, buf, t, w1, w2b, p.rtw1, p.rtw2);
+  FFT::template run<false, true>(v, buf, t, w1, w2b, t2);
   OMEGA_STAMP(2);
   // this thread's chroma records (group-ordered, j = cjf + kGrp i): the first two issued now, the
   // next ones once the transform's registers are free (after the threshold barrier), so the
@@ -498,7 +356,7 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   int cjf = cj0 + t % kGrp;
   static_for<0, kRecPre>([&](auto i) {
     const int j = cjf + kGrp * i;
-    if (kSpecPrefetch && j < cj1) {
+    if (j < cj1) {
       ra[i] = p.crec[2 * j];
       rb[i] = p.crec[2 * j + 1];
     }
@@ -515,11 +373,7 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
     const float2* bm = buf + FFT::s3m(t);
     static_for<0, 16>([&](auto q) {
       const float2 a = bo[FFT::o3(q)];
-      float2 b;
-      if constexpr (kSpecTight && q == 0)
-        b = t == 0 ? a : bm[FFT::o3(15)];  // t = 0: slot K would lie past the tight buffer (value unused)
-      else
-        b = bm[FFT::o3(15 - q)];
+      const float2 b = bm[FFT::o3(15 - q)];
       float2 xk, xkk;
       untangle(a, b, twc<q, 32>(wm), xk, xkk);
       mg[q] = cabs(xk);
@@ -545,14 +399,9 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
   for (int w = 1; w < NTH / 64; ++w) thr = fmaxf(thr, redf[w]);
   thr *= 0.1f;  // np.max(fft) * 0.1 in float32
   if (p.chroma_out && t < 12 * kGrp) {
-    if constexpr (!kSpecPrefetch) {
-      cj0 = p.cgoff[t / kGrp];
-      cj1 = p.cgoff[t / kGrp + 1];
-      cjf = cj0 + t % kGrp;
-    }
     static_for<0, kRecReg>([&](auto i) {
       const int j = cjf + kGrp * i;
-      if ((i >= kRecPre || !kSpecPrefetch) && j < cj1) {
+      if (i >= kRecPre && j < cj1) {
         ra[i] = p.crec[2 * j];
         rb[i] = p.crec[2 * j + 1];
       }
@@ -585,13 +434,6 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
     static_for<0, 2>([&](auto j) {
       const int i = t + NTH * j;
       if (i < p.n_out) {
-        if constexpr (!kSpecPrefetch) {
-          if (i < p.n_valid) {
-            bs[j] = p.starts[i];
-            be[j] = p.ends[i];
-            if (p.scale) bsc[j] = p.scale[i];
-          }
-        }
         band(i, bs[j], be[j], bsc[j]);
       }
     });
@@ -699,12 +541,8 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
 hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s) {
   // a suppressed bin k < c_hi names bin k / h >= k / 2, which must lie in the peak bitmap
   if (m != 8192 || (p.chroma_out && p.c_hi > 2 * 64 * kSpecRfPeakWords)) return hipErrorInvalidValue;
-  static const int pad = [] {  // development knob: extra dynamic LDS per workgroup (occupancy probe)
-    const char* e = std::getenv("OMEGA_SPEC_LDS_PAD");
-    return e ? std::atoi(e) : 0;
-  }();
-  using FFT = RegFFT<4096, kSpecTight>;
-  const size_t lds = FFT::kSlots * sizeof(float2) + (kSpecTight ? 0 : 8 * sizeof(float2)) + pad;
+  using FFT = RegFFT<4096>;
+  const size_t lds = (FFT::kSlots + 8 + FFT::kT2) * sizeof(float2);
   hipLaunchKernelGGL(spectra_rf_kernel<4096>, dim3((unsigned)p.n), dim3(kSpecRfThreads), lds, s, p);
   return hipGetLastError();
 }
@@ -744,13 +582,8 @@ __device__ __forceinline__ void batch_multi(const SpectralParams& p, int r, int6
 }
 
 // K-weighting role (kweight_kernel's LDS, carved: pwl 3 KiB | fbuf 64 KiB | sh 32 floats | edge 20
-// floats | red 8 doubles). OMEGA_BATCH_KW_NOINLINE: a call with its own register allocation.
-#ifdef OMEGA_BATCH_KW_NOINLINE
-__device__ __attribute__((noinline))
-#else
-__device__ __forceinline__
-#endif
-void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
+// floats | red 8 doubles)
+__device__ __forceinline__ void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
   constexpr int kP = 2 * kPwl * 16;  // pwl bytes
   auto* pwl = reinterpret_cast<float4(*)[kPwl]>(smem);
   float* fbuf = reinterpret_cast<float*>(smem + kP);
@@ -764,66 +597,10 @@ void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
   kw_count_in(kp, tid);
 }
 
-#if OMEGA_BATCH_EXTRAS
-// bounded poll of one lane: (int)(*ctr - target) >= 0, expiry -> err_word[1]
-__device__ __forceinline__ void batch_wait(const unsigned* ctr, unsigned target, int limit, unsigned* err) {
-  bool met = false;
-  for (int i = 0; i < limit; ++i) {
-    if ((int)(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) {
-      met = true;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(4);
-  }
-  if (!met && err) __hip_atomic_store(err + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// The true-peak meter (professional_meters.py:265-279: max over the last peak_len true peaks of the
-// stream, history ++ batch) for every (frame, channel) of the batch and the stream's true-peak history
-// rolled -- meter_query_kernel's true-peak part as the batch's last role. Per channel the sequence
-// history ++ batch is staged in LDS (one coalesced pass), then one thread per frame takes its window max.
-__device__ __forceinline__ void batch_tp_meter(const SpectralParams& sp, const BatchPlan& bp, int tid, char* smem) {
-  const MeterPrepParams& p = bp.mq;
-  if (tid == 0) {
-    batch_wait(sp.tp_done, bp.tp_target, bp.poll_limit, bp.err_word);
-    batch_wait(bp.join_ctr, bp.join_target, bp.poll_limit, bp.err_word);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-  float* seq = reinterpret_cast<float*>(smem);  // nt + F <= HT + kMeterChunk floats
-  const int C = p.C;
-  const int F = (int)p.n_frames;
-  for (int c = 0; c < C; ++c) {
-    const int nt = p.n_t_in[c];
-    const int tt = nt + F;
-    for (int i = tid; i < tt; i += kBatchThreads)
-      seq[i] = i < nt ? p.hist_t_in[(int64_t)c * p.HT + i] : p.tp[(int64_t)(i - nt) * C + c];
-    __syncthreads();
-    const int ktl = min(p.HT, tt);
-    for (int i = tid; i < ktl; i += kBatchThreads) p.hist_t_out[(int64_t)c * p.HT + i] = seq[tt - ktl + i];
-    if (tid == 0) p.n_t_out[c] = ktl;
-    for (int f = tid; f < F; f += kBatchThreads) {
-      const int ntp = nt + f + 1, wt = min(p.peak_len, ntp);
-      float tpm = -INFINITY;
-      for (int i = ntp - wt; i < ntp; ++i) tpm = fmaxf(tpm, seq[i]);
-      p.out[((int64_t)f * C + c) * 5 + 4] = (double)tpm;
-    }
-    __syncthreads();  // (seq is restaged for the next channel)
-  }
-}
-
-#endif
-
 __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, char* smem) {
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
   OMEGA_WG_BEGIN();
-#if OMEGA_BATCH_EXTRAS
-  if (b == bp.tpm_wg) {
-    batch_tp_meter(sp, bp, tid, smem);
-    return;
-  }
-#endif
   if (b < bp.seg_begin[2]) {
     const int sg = b < bp.seg_begin[1] ? 0 : 1;
     const int j = b - bp.seg_begin[sg], nr = bp.n_roles[sg];
@@ -861,29 +638,6 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
 __global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams sp, KWeightParams kp, BatchPlan bp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   batch_body(sp, kp, bp, smem);
-#if OMEGA_BATCH_EXTRAS
-  if (bp.wg_done) {
-    // the join: the workgroup that finishes the launch's count waits for the side stream's meter
-    // queries, so this stream completes after them (no stream event, no kernel after the batch)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned old = __hip_atomic_fetch_add(bp.wg_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (old + 1u == bp.wg_target) {
-        bool met = false;
-        for (int i = 0; i < bp.poll_limit; ++i) {
-          if ((int)(__hip_atomic_load(bp.join_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - bp.join_target) >= 0) {
-            met = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(4);
-        }
-        if (!met && bp.err_word)
-          __hip_atomic_store(bp.err_word + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
-    }
-  }
-#endif
 }
 
 hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s) {

@@ -223,23 +223,10 @@ hipError_t launch_mrfft_range(const SpectralParams& p, int r0, int r1, hipStream
   return hipSuccess;
 }
 
-// The true-peak kernel for frames of W samples.
-template <int K, int NTH = threads_for<K>()>
-__global__ __launch_bounds__(NTH, 2 * NTH / 256) void truepeak_l2_kernel(SpectralParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  truepeak_l2_body<K, NTH>(p, blockIdx.x, threadIdx.x, reinterpret_cast<float2*>(smem),
-                           reinterpret_cast<float*>(smem + K * sizeof(float2)));
-}
-
 OMEGA_STAMPS_GETTER(omega_debug_spectral_stamps)
 
 hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
-  if (p.tp_out && W == 16384 && p.tp_scratch) {
-    hipLaunchKernelGGL(truepeak_l2_kernel<8192>, grid, dim3(threads_for<8192>()), 8192 * sizeof(float2) + 16 * sizeof(float),
-                       s, p);
-    return hipGetLastError();
-  }
   if (p.tp_out) {
 #define OMEGA_TP(K) \
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&truepeak_kernel<K>), \

@@ -1,5 +1,5 @@
 // Spectral device code shared by the spectral kernels (spectral.hip) and the fused frame kernel
-// (frame.hip): real-FFT magnitudes, the per-resolution frame body (A3-A5) and the true-peak body
+// (the cfg2 role kernels): real-FFT magnitudes, the per-resolution frame body (A3-A5) and the true-peak body
 // (A8). See spectral.hip for the algorithms. Include after OMEGA_STAMPS_DECL.
 #pragma once
 #include "fft.hpp"
@@ -229,87 +229,6 @@ __device__ __forceinline__ void truepeak_body(const SpectralParams& p, int64_t c
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
   if (tid == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
   OMEGA_STAMP(9);
-}
-
-// True peak with the spectrum parked in global memory instead of registers: 512 threads, the
-// in-place radix-16 plan, 64 KiB of LDS -- two workgroups per CU, whose barrier phases interleave.
-// The pairs (X_k, X_{K-k}) of thread t sit at xs[b * NTH + t] (coalesced float4, written once and
-// read back by the same workgroup in each phase, so they stay in L2). Each phase P multiplies them
-// by r_k^P and q_k^P (r_k = e^{2 pi i k / 4M}, q_k = e^{i pi/4} conj r_k).
-template <int K, int NTH>
-__device__ __forceinline__ void truepeak_l2_body(const SpectralParams& p, int64_t cf, int tid, float2* buf, float* red) {
-  constexpr int M = 2 * K;
-  using FFT = BlockFFT<K, NTH>;
-  const int64_t f = cf / p.C, c = cf % p.C;
-  const float2* x2 = reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride);
-  float4* __restrict__ xs = p.tp_scratch + cf * (K / 2);
-  float mx = 0.f;  // p = 0 phase: the samples themselves
-  const typename FFT::Tw tw = FFT::load_tw(p.tw[ilog2(K)], tid);
-  FFT::run_from(buf, tw, tid, [&](int i) {
-    const float2 a = x2[i];
-    mx = fmaxf(mx, fmaxf(fabsf(a.x), fabsf(a.y)));
-    return a;
-  });
-  const float2* __restrict__ twM = p.tw[ilog2(M)];
-  constexpr int NP = K / 2;
-  constexpr int PB = NP / NTH;
-  static_assert(NP % NTH == 0, "pairs per thread");
-  float2 Xmid = make_float2(0.f, 0.f);
-  static_for<0, PB>([&](auto b) {
-    const int k = tid + b * NTH;
-    const int kk = k == 0 ? K / 2 : K - k;
-    const float2 a = buf[FFT::out(k)], bz = buf[FFT::out(kk)];
-    float2 lo, hi;
-    untangle(a, bz, twM[k], lo, hi);
-    if (k == 0) Xmid = cconj(bz);
-    lo = k == 0 ? make_float2(a.x + a.y, 0.f) : lo;
-    hi = k == 0 ? make_float2(a.x - a.y, 0.f) : hi;
-    xs[b * NTH + tid] = make_float4(lo.x, lo.y, hi.x, hi.y);
-  });
-  const float2* __restrict__ rot = p.rot;
-  const float2 rh = rot[K / 2];
-  constexpr float kS2 = 7.071067812e-01f;
-  float fmx = 0.f;
-#pragma unroll 1
-  for (int P = 1; P <= 3; ++P) {
-    int tl = tid;
-    typename FFT::Tw twl = tw;
-    twl.launder();
-    asm volatile("" : "+v"(tl));
-    __syncthreads();  // the previous transform's last pass has read buf
-    if (!((p.tp_phases >> P) & 1)) {  // phase not requested: only the running Nyquist-mirror rotation
-      if (tl == 0) Xmid = cmul(Xmid, rh);
-      continue;
-    }
-    static_for<0, PB>([&](auto b) {
-      const int k = tl + b * NTH;
-      const float4 xp = xs[b * NTH + tl];
-      const float2 r1 = rot[k];
-      const float2 r2 = cmul(r1, r1);
-      const float2 rp = P == 1 ? r1 : (P == 2 ? r2 : cmul(r2, r1));
-      const float2 e = cmul(r2, r2);  // e^{2 pi i k / M}
-      const float2 q1 = make_float2(kS2 * (r1.x + r1.y), kS2 * (r1.x - r1.y));
-      const float2 q2 = cmul(q1, q1);
-      const float2 qp = P == 1 ? q1 : (P == 2 ? q2 : cmul(q2, q1));
-      const float2 yk = cmul(make_float2(xp.x, xp.y), rp);
-      const float2 yh = cmul(make_float2(xp.z, xp.w), qp);
-      // k = 0 carries the Nyquist bin X_K (real): its share is Re(X_K e^{i pi P/4})
-      const float2 ykk = (k == 0) ? make_float2(yh.x, 0.f) : yh;
-      const float2 E = make_float2(0.5f * (yk.x + ykk.x), 0.5f * (yk.y - ykk.y));
-      const float2 O = cmul(make_float2(0.5f * (yk.x - ykk.x), 0.5f * (yk.y + ykk.y)), e);
-      buf[k] = make_float2(E.x - O.y, -(E.y + O.x));
-      if (k != 0) {
-        buf[K - k] = make_float2(E.x + O.y, E.y - O.x);
-      } else {
-        Xmid = cmul(Xmid, rh);
-        buf[K / 2] = Xmid;
-      }
-    });
-    __syncthreads();
-    FFT::run_to(buf, twl, tl, [&](int, float2 z) { fmx = fmaxf(fmx, fmaxf(fabsf(z.x), fabsf(z.y))); });
-  }
-  const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
-  if (tid == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
 }
 
 }  // namespace omega

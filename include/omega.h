@@ -130,10 +130,9 @@ int omega_set_stream(omega_ctx* ctx, void* hip_stream);
  * see DESIGN.md); bits 1-2 = stream layout:
  * 0 default: 16384-sample frames on direct launches run as ONE batch kernel (K-weighting, true peak
  * and every resolution as workgroup roles of one grid) with the meter aggregates on a side stream that
- * is ordered by device counters instead of stream events; other calls (and graph capture) as 3;
- * 1 everything sequentially on one stream; 2 three concurrent branches (resolution kernels / true
- * peak / K-weighting + meters); 3 the full-chip kernels back to back on the stream, the latency-bound
- * meter prep and LUFS query kernels on a side stream joined by events. */
+ * is ordered by device counters instead of stream events; other calls (and graph capture) as below;
+ * any other value: the full-chip kernels back to back on the stream, the latency-bound meter prep and
+ * LUFS query kernels on a side stream joined by events. Every layout gives the same outputs bitwise. */
 int omega_set_graphs(omega_ctx* ctx, int flags);
 /* The stream calls enqueue on (omega_set_stream), and the context's configuration and device. */
 void* omega_get_stream(const omega_ctx* ctx);

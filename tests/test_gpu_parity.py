@@ -606,7 +606,7 @@ def test_stream_layout_hop(cfg2):
 def test_meter_chunks_across_layouts():
     """A batch longer than one meter chunk (kMeterChunk = 2048 frames): the default layout (meter
     prep + LUFS meters on a side stream, the true-peak meter on the main one, chunk by chunk) gives
-    the sequential layout's meters bitwise, and a frame past the chunk boundary matches the oracle's
+    the side-meter kernel layout's and the graph path's meters bitwise, and a frame past the chunk boundary matches the oracle's
     sequential calculate_lufs calls."""
     import torch
     from omega_gpu import Engine, Resolution
@@ -616,7 +616,7 @@ def test_meter_chunks_across_layouts():
     x = torch.from_numpy(np.stack([S.sine(330, 0.3, n) * (1 + 0.5 * np.sin(np.arange(n) / 9000.0)),
                                    S.noise(5, n, 0.1)]).astype(np.float32).ravel()).cuda()
     res = []
-    for flags in (1, 2, 0):  # graphs + default, direct + sequential, direct + default
+    for flags in (1, 2, 0):  # graphs, direct + side-meter kernels, direct + default
         eng = Engine([Resolution((20, 20000), 1024, 256, 1.0)], FS, 20000, 64, n_channels=2)
         eng._check(L.lib().omega_set_graphs(eng._ctx, flags))
         o = eng.process_stream(x, n, H, channel_stride=n, combined=False, meters=True)
@@ -642,24 +642,17 @@ def test_zero_frames_is_noop():
 
 def test_graph_replay_matches_direct_launch():
     """Device-memory calls are captured into HIP graphs and replayed; over several consecutive batches
-    (meter state ping-pong included) the replayed path equals direct launches bitwise. The sequential
-    layout and the fused frame kernel (K-weighting in 16-sample scan chunks, another compilation of
-    the true-peak body) agree with it bitwise on spectra, within float32 rounding on TP and LUFS."""
+    (meter state ping-pong included) the replayed path equals direct launches of the same kernels and
+    the default one-launch batch layout bitwise."""
     import torch
     from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
     from omega_gpu import _lib as L
     x = torch.from_numpy(S.cfg2_batch(8)).cuda()
     outs = []
-    import os
-    for flags, fuse in ((1, "0"), (6, "0"), (2, "0"), (1, "1"), (5, "0"), (0, "0")):
-        # graphs (captured: full-chip kernels back to back, meters on a side stream), the same layout
-        # on direct launches, direct + sequential, graphs + fused frame kernel, graphs + three
-        # concurrent branches, direct + default (one batch_kernel launch)
-        os.environ["OMEGA_FUSE"] = fuse
-        try:
-            eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
-        finally:
-            del os.environ["OMEGA_FUSE"]
+    for flags in (1, 2, 0, 3):
+        # graphs (captured: full-chip kernels back to back, meters on a side stream), the same layout on
+        # direct launches, direct + default (one batch_kernel launch), graphs with the layout bits set
+        eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
         eng._check(L.lib().omega_set_graphs(eng._ctx, flags))
         bufs = [{k: torch.empty(16, *s, dtype=d, device="cuda") for k, s, d in
                  (("combined", (512,), torch.float32), ("lufs_inst", (), torch.float32),
@@ -670,14 +663,10 @@ def test_graph_replay_matches_direct_launch():
             torch.cuda.synchronize()
             seq.append({k: v.clone() for k, v in o.items()})
         outs.append(seq)
-    for a, b in [*zip(outs[0], outs[1]), *zip(outs[0], outs[5])]:
-        for k in a:
-            assert torch.equal(a[k], b[k]), k
-    for a, c in [*zip(outs[0], outs[2]), *zip(outs[0], outs[3]), *zip(outs[0], outs[4])]:
-        assert torch.equal(a["combined"], c["combined"])
-        assert torch.max(torch.abs(a["true_peak_db"] - c["true_peak_db"])).item() < 1e-4
-        assert torch.max(torch.abs(a["lufs_inst"] - c["lufs_inst"])).item() < 1e-3
-        assert torch.max(torch.abs(a["meters"] - c["meters"])).item() < 1e-3
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            for k in a:
+                assert torch.equal(a[k], b[k]), k
 
 
 def test_batch_layout_ragged_and_partial_outputs():
@@ -946,7 +935,7 @@ def test_app_post_ema_slow_factors_exact():
 
     def slow_ref(*a):
         keep, f = orig_ref(*a)
-        return keep, list(np.linspace(0.9, 0.995, len(f)))
+        return keep, [float(v) for v in np.linspace(0.9, 0.995, len(f))]  # Python floats, as the app's
     try:
         AP._band_table, R.app_band_table = slow_dev, slow_ref
         _, b, _ = AP.SpectrumPostProcessor(freqs).process(x)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Kernel-variant probe on the development library (make -C audio-analyzer-omega_amd dev):
-python tools/probe.py --which 0 1 [--frames F] -- times omega_dev_probe(which) over F stereo cfg2
+python tools/probe.py --which 0 2 [--frames F] -- times omega_dev_probe(which) over F stereo cfg2
 frames (HIP events, back-to-back launches) and checks every variant's outputs against variant 0's."""
 import argparse
 import ctypes as C
@@ -19,7 +19,7 @@ _L.use_development_library("libomega_dev.so")
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", type=int, nargs="+", default=[0, 1])
+    ap.add_argument("--which", type=int, nargs="+", default=[0, 2])
     ap.add_argument("--frames", type=int, nargs="+", default=[256, 4096])
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
