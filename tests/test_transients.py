@@ -96,3 +96,25 @@ def test_transients_sizes_vs_oracle(n):
     z = ta.analyze_transients(np.zeros(3000))  # a length off the packed transform (transient_any_kernel)
     assert z == {"transients_detected": 0, "attack_time": 0.0, "punch_factor": 0.0, "envelope_peak": 0.0,
                  "envelope_rms": 0.0}
+
+
+@pytest.mark.gpu
+def test_transients_any_length_sliced_scratch():
+    """Frames too long for LDS run on global working buffers in slices of frames (64 MiB of scratch
+    per launch): 420 frames of 10000 samples span three slices (209 frames each) and equal the same
+    frames analysed in single-frame calls bitwise; a few frames against the oracle to float32 rounding."""
+    from omega_gpu.transient import TransientAnalyzer
+    rng = np.random.default_rng(42)
+    n, F = 10000, 420
+    x = (rng.standard_normal((F, n)) * np.linspace(0.05, 0.9, F)[:, None]).astype(np.float32)
+    x[:, 3000:3050] *= 8.0
+    ta = TransientAnalyzer(48000)
+    got = ta.analyze_batch(x)
+    for f in (0, 208, 209, 210, 418, 419):
+        one = TransientAnalyzer(48000).analyze_batch(x[f:f + 1])
+        np.testing.assert_array_equal(got[f], one[0], err_msg=str(f))
+    st = R.TransientState(48000)
+    for f in (0, 209, 419):
+        r = st.analyze(x[f])
+        assert got[f, 0] == r[KEYS[0]]
+        np.testing.assert_allclose(got[f, 1:5], [r[k] for k in KEYS[1:5]], rtol=1e-6, atol=1e-12)

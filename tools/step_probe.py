@@ -2,7 +2,7 @@
 """Step time of the cfg2 workload per stream layout (omega_set_graphs flags), with the host's enqueue
 cost per call next to it (is the step host-bound?).
 
-  python tools/step_probe.py [--steps N] [--modes 0,6,...]
+  python tools/step_probe.py [--steps N] [--modes 0,2,...] [--lib libomega_ab.so]
 """
 import argparse
 import ctypes
@@ -15,15 +15,18 @@ sys.path.insert(0, os.path.join(REPO, "audio-analyzer-omega_amd"))
 sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
-NAMES = {0: "direct/default", 1: "graph/default", 2: "direct/sequential", 4: "direct/concurrent",
-         6: "direct/side-meters", 7: "graph/side-meters"}
+NAMES = {0: "direct/default", 1: "graph", 2: "direct/side-meters"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--modes", default="0,6,1")
+    ap.add_argument("--modes", default="0,2,1")
+    ap.add_argument("--lib", default=None, help="another build in lib/ (A/B of two builds on one box)")
     a = ap.parse_args()
+    if a.lib:
+        from omega_gpu import _lib as L0
+        L0.use_development_library(a.lib)
     import bench
     from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
     from omega_gpu import _lib as L

@@ -18,7 +18,7 @@ from omega_gpu import _lib as _L  # noqa: E402
 
 _L.use_development_library("libomega_dev.so")
 
-ROLE = {0: "kw", 1: "tp", 2: "res16k", 11: "tp_pair", 12: "res16k_pair", 3 + 512: "res512", 3 + 1024: "res1k", 3 + 2048: "res2k",
+ROLE = {0: "kw", 1: "tp", 2: "res16k", 20: "spectra", 3 + 512: "res512", 3 + 1024: "res1k", 3 + 2048: "res2k",
         3 + 4096: "res4k", 3 + 8192: "res8k"}
 
 
@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--probe", type=int, default=None, help="trace omega_dev_probe(which) instead of the batch")
+    ap.add_argument("--cfg3", action="store_true", help="trace the cfg3 spectra kernel (4096 frames of 8192)")
     a = ap.parse_args()
     import bench
     from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
@@ -45,8 +46,17 @@ def main():
         pf.restype = C.c_int
         pf.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
         aux = torch.zeros(ncf * 4, device="cuda")
+    if a.cfg3:
+        from omega_gpu import Resolution
+        from omega_gpu.engine import BandTable
+        x3 = torch.from_numpy(bench.cfg3_input(4096, 8192)).cuda()
+        e3 = Engine([Resolution((20, 20000), 8192, 2048, 1.0)], 48000, 20000, 512)
+        st_, en_, comp_ = bench.band_table_512()
+        bt = BandTable(e3, L.BANDS_MAX, st_, en_, 512, 4097, scale=comp_)
     for _ in range(a.reps):
-        if a.probe is not None:
+        if a.cfg3:
+            e3.spectra(x3, "hann", bands=bt, chroma=True)
+        elif a.probe is not None:
             eng._check(pf(eng._ctx, a.probe, x.data_ptr(), F, keep[0].data_ptr(), aux.data_ptr()))
         else:
             eng._check(lib.omega_process_frames(eng._ctx, x.data_ptr(), F, 2 * 16384, 16384, C.byref(outs), L.MEM_DEVICE))
