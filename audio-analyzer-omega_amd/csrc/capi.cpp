@@ -216,7 +216,6 @@ struct omega_ctx {
   unsigned* d_kw_done = nullptr;  // batch_kernel's K-weighting workgroups count themselves in here
   unsigned kw_issued = 0;         // K-weighting workgroups launched with the count on (wraps)
   unsigned q_issued = 0;          // LUFS-meter query workgroups launched with the count on (d_kw_done[1])
-  unsigned tp_issued = 0;         // batch true-peak workgroups launched with the count on (d_kw_done[2])
   // device-side poll expiry flags (host-mapped: [0] meter prep, [1] join), checked by
   // check_device_err; the poll bound (OMEGA_POLL_LIMIT, a test knob)
   unsigned* h_err = nullptr;
@@ -675,7 +674,7 @@ int build_meter_state(omega_ctx* c) {
     HIPC(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_err), c->h_err, 0));
   }
   HIPC(c, hipMemset(c->d_kw_done, 0, 8 * sizeof(unsigned)));
-  c->kw_issued = c->q_issued = c->tp_issued = 0;
+  c->kw_issued = c->q_issued = 0;
   return omega_meter_reset(c);
 }
 
@@ -830,17 +829,17 @@ bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams&
 }
 
 // The default layout for 16384-sample frames. On `s`: one batch_kernel launch (BatchPlan: K-weighting
-// and 16384-point-resolution workgroups mixed, then the true peaks, then the small resolutions). On
-// fork[0]: the meter prep (it waits on the K-weighting count, kw_done) and the LUFS meters (their
-// workgroups count themselves in). The true-peak meter: with one meter chunk inside the batch (the last
-// true-peak workgroup, BatchPlan::tpm), otherwise a kernel after it on `s`; either waits for the LUFS
+// and 16384-point-resolution workgroups mixed, then the true peaks, then the small resolutions) and the
+// true-peak meter. On fork[0]: the meter prep (it waits on the K-weighting count, kw_done) and the LUFS
+// meters (their workgroups count themselves in). The true-peak meter's first workgroup waits for that
 // count, so `s` completes only after fork[0]'s work: no stream events anywhere (each event record /
 // wait cost ~7-13 us of idle GPU between kernels). Mixing the latency-bound K-weighting scans with
 // transform work is what pays (K-weighting alone 25.7 us, the true peak 37, the resolutions 26.5; one
 // batch launch of all three 73.9). Measured and rejected on MI355X (round 1-2): other role
 // orders (K-weighting as its own kernel 110.4 us per step; mixed with the true peaks 85.2; the true
 // peaks first ~equal), the meter queries after the batch (88 vs 81-82), the true-peak query on the side
-// stream joined in the batch's last workgroup (85-87), the true-peak meter as a batch role (86-88).
+// stream joined in the batch's last workgroup (85-87), the true-peak meter as a batch role (86-88), the
+// true-peak meter by the batch's last true-peak workgroup, joined there (86.2 vs 81.1, round 3).
 int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
                   const float* tp, double* meters, hipStream_t s, int mr, bool do_tp, bool do_kw) {
   (void)W;
@@ -877,13 +876,10 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   const int64_t grid = end + nwg;
   if (grid > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
   std::vector<MeterPrepParams> mc;
-  bool tail = false;
   if (meters) {
     mc = meter_chunks(c, lufs, tp, n_frames, meters);
     kp.kw_done = c->d_kw_done;
     c->kw_issued += (unsigned)n;
-    // one meter chunk: the true-peak meter inside the batch (BatchPlan::tpm), no kernel after it
-    tail = do_tp && mc.size() == 1 && mc[0].tp == sp.tp_out;
     for (size_t i = 0; i < mc.size(); ++i) {
       MeterPrepParams p = mc[i];
       if (i == 0) {
@@ -897,38 +893,15 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
       c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);  // (counted once it is enqueued)
     }
   }
-  if (tail) {
-    const MeterPrepParams& p = mc[0];
-    sp.tp_done = c->d_kw_done + 2;
-    c->tp_issued += (unsigned)n;
-    TpMeterTail& q = bp.tpm;
-    q.tp = p.tp;
-    q.hist_in = p.hist_t_in;
-    q.hist_out = p.hist_t_out;
-    q.n_in = p.n_t_in;
-    q.n_out = p.n_t_out;
-    q.out = p.out;
-    q.F = (int)p.n_frames;
-    q.C = p.C;
-    q.HT = p.HT;
-    q.peak_len = p.peak_len;
-    q.tp_target = c->tp_issued;
-    q.join_ctr = c->d_kw_done + 1;
-    q.join_target = c->q_issued;
-    q.poll_limit = c->poll_limit;
-    q.err_word = c->d_err;
-  }
   if (grid > 0) {
     const hipError_t le = launch_batch(sp, kp, bp, (int)grid, s);
     if (le != hipSuccess) {
-      // the prep kernel already waits for this batch's count: publish it (and the true-peak count), so
-      // that every later call's target stays in step with the device counters instead of timing out
+      // the prep kernel already waits for this batch's count: publish it, so that it (and every later
+      // call's target) stays in step with the device counter instead of timing out
       if (meters) (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
-      if (tail) (void)hipMemcpy(c->d_kw_done + 2, &c->tp_issued, sizeof(unsigned), hipMemcpyHostToDevice);
       return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
     }
   }
-  if (tail) return 0;
   for (size_t i = 0; i < mc.size(); ++i) {
     MeterPrepParams p = mc[i];
     p.parts = 2;

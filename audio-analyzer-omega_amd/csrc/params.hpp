@@ -48,7 +48,7 @@ struct SpectralParams {
   const float2* tw[kMaxLog2];  // tw[l][m] = exp(-2 pi i m / 2^l)
   int rf_sizes;  // host-side launch choice: bit log2(N) set = resolution size N runs on the register-FFT kernel
   // batch_kernel's true-peak role: when set, the value is stored write-through and the workgroup adds 1
-  // after it (BatchPlan::tpm: the last one to count in computes the true-peak meter)
+  // after it (the true-peak meter query on the side stream waits for the batch's count)
   unsigned* tp_done;
 };
 
@@ -206,35 +206,12 @@ struct MultiPlan {
 //       the roles of a frame land on one XCD (blockIdx % 8) and a CU sees the roles mixed
 //   [seg_begin[2], ...)  the resolutions of at most 8192 points (multi; wg_begin relative to seg_begin[2])
 // The K-weighting role counts itself into KWeightParams::kw_done when that is set.
-//
-// The true-peak meter of the batch (one meter chunk, out != nullptr): every true-peak workgroup stores
-// its value write-through and counts into SpectralParams::tp_done; the one whose count completes the
-// batch (old + 1 == tp_target) computes column 4 of the meters for every (frame, channel) -- the max
-// over the last peak_len true peaks of history ++ batch (professional_meters.py:265-279) -- and rolls
-// the true-peak history, then waits (bounded) until the side stream's LUFS queries have counted in
-// (join_ctr >= join_target), so that the launch completes after them: no kernel after the batch.
-struct TpMeterTail {
-  const float* tp;  // [F * C] the batch's true peaks (SpectralParams::tp_out)
-  const float* hist_in;
-  float* hist_out;  // [C, HT]
-  const int* n_in;
-  int* n_out;       // [C]
-  double* out;      // [F * C, 5], column 4
-  int F, C, HT, peak_len;
-  unsigned tp_target;
-  unsigned* join_ctr;
-  unsigned join_target;
-  int poll_limit;
-  unsigned* err_word;  // expiry of the join poll -> err_word[1]
-};
-
 struct BatchPlan {
   int seg_begin[3];
   int n_roles[2];
   int roles[2][3];
   int mr_res;
   MultiPlan multi;
-  TpMeterTail tpm;
 };
 
 // Fused spectrum analysis (cfg3): windowed rfft magnitude (A13) -> log-band max (A10) and raw

@@ -51,9 +51,8 @@ __device__ __forceinline__ int tp_column(int tid) {
   return a == 0 ? NTH / 2 : NTH - a;
 }
 
-// Returns, on thread 0 when p.tp_done is set, the count before this workgroup's add.
 template <int K>
-__device__ __forceinline__ unsigned truepeak_rf_body(const SpectralParams& p, int64_t cf, int tid, char* smem) {
+__device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_t cf, int tid, char* smem) {
   using FFT = RegFFT<K>;
   constexpr int NTH = FFT::NTH, M = 2 * K;
   const int t = tp_column<NTH>(tid);  // this thread's spectrum column (pass-1 input, untangle, phases)
@@ -154,19 +153,17 @@ __device__ __forceinline__ unsigned truepeak_rf_body(const SpectralParams& p, in
     OMEGA_STAMP(4 + 4 * P);
   }
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
-  unsigned old = 0;
   if (tid == 0) {
     const float db = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
     if (p.tp_done) {  // write-through, drained, then counted in (see SpectralParams::tp_done)
       __hip_atomic_store(reinterpret_cast<unsigned*>(p.tp_out + cf), __float_as_uint(db), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      old = __hip_atomic_fetch_add(p.tp_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(p.tp_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       p.tp_out[cf] = db;
     }
   }
-  return old;
 }
 
 template <int K>
@@ -590,44 +587,6 @@ __device__ __forceinline__ void batch_multi(const SpectralParams& p, int r, int6
   mrfft_frame<K, G>(p, r, valid ? cf : p.n_cf - 1, valid, tid % G, smem + grp * K);
 }
 
-// The true-peak meter of the batch (BatchPlan::tpm) by the last true-peak workgroup: per channel the
-// sequence history ++ batch staged in LDS (one coalesced pass), the history rolled, then one thread per
-// frame takes its window max (meter_query_body's true-peak part); then the join with the side stream.
-__device__ __forceinline__ void batch_tp_meter(const TpMeterTail& q, int tid, char* smem) {
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other workgroups' write-through true peaks
-  float* seq = reinterpret_cast<float*>(smem);      // nt + F <= HT + kMeterChunk floats
-  const int C = q.C, F = q.F;
-  for (int c = 0; c < C; ++c) {
-    const int nt = q.n_in[c];
-    const int tt = nt + F;
-    for (int i = tid; i < tt; i += kBatchThreads)
-      seq[i] = i < nt ? q.hist_in[(int64_t)c * q.HT + i] : q.tp[(int64_t)(i - nt) * C + c];
-    __syncthreads();
-    const int ktl = min(q.HT, tt);
-    for (int i = tid; i < ktl; i += kBatchThreads) q.hist_out[(int64_t)c * q.HT + i] = seq[tt - ktl + i];
-    if (tid == 0) q.n_out[c] = ktl;
-    for (int f = tid; f < F; f += kBatchThreads) {
-      const int ntp = nt + f + 1, wt = min(q.peak_len, ntp);
-      float m = -INFINITY;
-      for (int i = ntp - wt; i < ntp; ++i) m = fmaxf(m, seq[i]);
-      q.out[((int64_t)f * C + c) * 5 + 4] = (double)m;
-    }
-    __syncthreads();  // (seq is restaged for the next channel)
-  }
-  if (tid == 0) {
-    bool met = false;
-    for (int i = 0; i < q.poll_limit; ++i) {
-      if ((int)(__hip_atomic_load(q.join_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - q.join_target) >= 0) {
-        met = true;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(4);
-    }
-    if (!met && q.err_word) __hip_atomic_store(q.err_word + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-}
-
 // K-weighting role (kweight_kernel's LDS, carved: pwl 3 KiB | fbuf 64 KiB | sh 32 floats | edge 20
 // floats | red 8 doubles)
 __device__ __forceinline__ void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
@@ -657,15 +616,7 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
     if (role == 0) {
       batch_kw_role(kp, cf, tid, smem);
     } else if (role == 1) {
-      const unsigned old = truepeak_rf_body<8192>(sp, cf, tid, smem);
-      if (bp.tpm.out) {
-        // the flag lies past the exchange buffer (the last transform's reads are done; block_max's
-        // scratch is not touched), the meter's staging at its start
-        int* last = reinterpret_cast<int*>(smem + lds_bytes<8192>() - 16);
-        if (tid == 0) *last = old + 1u == bp.tpm.tp_target;
-        __syncthreads();
-        if (*last) batch_tp_meter(bp.tpm, tid, smem);
-      }
+      truepeak_rf_body<8192>(sp, cf, tid, smem);
     } else {
       mrfft_rf_body<8192>(sp, bp.mr_res, cf, tid, smem);
     }
