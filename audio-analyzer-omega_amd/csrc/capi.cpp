@@ -1459,12 +1459,21 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   p.spec_out = spectrum_out;
   p.band_out = bands_out;
   p.content_out = content_out;
-  if (c->post.nb) {  // (+ the EMA's spare rows: post.hip post_ema_kernel)
-    if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, (n_frames + kEmaSpareRows) * (c->post.nb + 1))) return e;
+  // scratch: the raw band rows (+ the EMA's spare rows: post.hip post_ema_kernel), the per-frame dtype
+  // flags, then (8-byte aligned) the EMA chunks' warm-up values at their boundaries, end values and
+  // boundary mismatch flags
+  const int64_t rows = n_frames + kEmaSpareRows, nch = (n_frames + 63) / 64;
+  const int64_t pre_off = (rows * (c->post.nb + 1) + 1) / 2 * 2;
+  const int64_t nchp = (nch + 15) / 16 * 16;
+  if (c->post.nb) {
+    if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, pre_off + 4 * nch * c->post.nb + nchp * c->post.nb / 4 + 4))
+      return e;
   }
   p.band_raw = c->d_post_raw;
-  // the per-frame dtype flags after the raw band rows
-  p.frame64 = reinterpret_cast<int*>(c->d_post_raw + (n_frames + kEmaSpareRows) * c->post.nb);
+  p.frame64 = reinterpret_cast<int*>(c->d_post_raw + rows * c->post.nb);
+  p.ema_pre = reinterpret_cast<double*>(c->d_post_raw + pre_off);
+  p.ema_end = p.ema_pre + nch * c->post.nb;
+  p.ema_flag = reinterpret_cast<unsigned char*>(p.ema_end + nch * c->post.nb);
   HIPC(c, launch_post(p, c->stream));
   if (c->post.nb) {  // the EMA wrote the other state buffer: it is the next call's input
     std::swap(c->post.prev, c->post.prev_out);

@@ -279,6 +279,11 @@ struct PostParams {
   double* band_out;            // [n, nb] (float32 values, or float64 on frames whose list held the int 1)
   float* band_raw;             // [n, nb] scratch: the clamped band values before the EMA
   int* frame64;                // [n] scratch: 1 where a band clamped to the Python int 1 (float64 array)
+  double* ema_pre;             // [n / 64 chunks, nb] scratch: each EMA chunk's warm-up value at the frame
+                               // before it (post.hip post_ema_kernel)
+  double* ema_end;             // [n / 64 chunks, nb] scratch: each chunk's value at its last frame
+  unsigned char* ema_flag;     // [nb, nchp] scratch: chunk boundary mismatch flags (nchp = chunks
+                               // rounded up to 16)
   int* content_out;            // [n]
   // EMA state {value, float64 dtype, present} in (double-buffered: the kernels read one, write the
   // other)

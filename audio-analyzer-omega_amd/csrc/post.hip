@@ -266,35 +266,43 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
 //   v = a + b          float64 if either is, stored into this frame's array (rounded to float32 there)
 // Every operation is rounded on its own (contraction off), so the device repeats numpy's results bit
 // for bit, denormals included (a decaying band sticks at the smallest denormal as it does on the CPU).
+// Branch-free: both products of each term, selected; the all-float32 case float32(a32 + b32) equals
+// float32(float64(a32) + float64(b32)) (float64 carries more than 2 x 24 + 2 bits, so rounding the
+// float64 sum again to float32 is innocuous), so one float64 add serves all four dtype combinations.
 struct EmaState {
   double v;
   bool f64;
 };
 __device__ __forceinline__ double ema_step(const EmaState& s, float x, bool x64, const EmaCoef& k) {
-  const double a = s.f64 ? s.v * k.f : (double)((float)s.v * k.f32);
-  if (s.f64 || x64) {
-    const double b = x64 ? (double)x * k.g : (double)(x * k.g32);
-    const double v = a + b;
-    return x64 ? v : (double)(float)v;
-  }
-  return (double)((float)a + x * k.g32);
+  const double a64 = s.v * k.f;
+  const double a32 = (double)((float)s.v * k.f32);
+  const double b64 = (double)x * k.g;
+  const double b32 = (double)(x * k.g32);
+  const double v = (s.f64 ? a64 : a32) + (x64 ? b64 : b32);
+  return x64 ? v : (double)(float)v;
 }
 
-// One thread per (band, chunk of kEmaChunk frames). The first chunk continues the stream's state; a
-// later chunk starts kEmaWarm frames early as at a stream start (no previous value) and runs the same
-// recurrence up to its own frames. Where the warm-up's start has faded out of every rounding (the usual
-// case) the chunk already holds the sequential values; post_ema_fix_kernel checks every chunk's first
-// value against the true state and re-runs the chunks where it differs (after a silence the true state
-// is still decaying while a warm-up from silent frames starts at 0). Loads go in blocks of kEmaBlock
-// frames, the next block's in flight during this block's recurrence.
+// One thread per (band, chunk of kEmaChunk frames). The first chunks (up to frame kEmaWarm) start at
+// the stream's state; a later chunk starts kEmaWarm frames early as at a stream start (no previous
+// value) and runs the same recurrence up to its own frames, recording its value at the frame before its
+// own (ema_pre). Where the warm-up's start has faded out of every rounding (the usual case) that value
+// equals the chunk before's stored one, and then (same operations on the same values from there on)
+// the chunk holds the sequential values; post_ema_fix_kernel re-runs the chunks where it differs. Loads
+// go in blocks of kEmaBlock frames, the next block's in flight during this block's recurrence; a block
+// whose frames all share the state's dtype runs the plain float64 or float32 recurrence (the frames'
+// dtype flags are the same on every lane: a uniform branch).
 constexpr int kEmaBlock = 32;
 static_assert(kEmaBlock <= kEmaSpareRows, "the spare rows cover a block");
 constexpr int kEmaChunk = 64;
 constexpr int kEmaWarm = 256;
 __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
-  const int b = blockIdx.x * 64 + threadIdx.x;
   const int64_t c0 = (int64_t)blockIdx.y * kEmaChunk;
-  if (b >= p.nb || c0 >= p.n) return;
+  if (c0 >= p.n) return;
+  // every lane stays (its flag load serves the block's dtype bits); lanes past the last band compute
+  // the last band's values and store nothing
+  const int bl = blockIdx.x * 64 + threadIdx.x;
+  const bool live = bl < p.nb;
+  const int b = live ? bl : p.nb - 1;
   const EmaCoef k = p.sf[b];
   const bool smooth = (p.flags & 8) != 0;
   const int64_t c1 = c0 + kEmaChunk < p.n ? c0 + kEmaChunk : p.n;
@@ -302,7 +310,7 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
   const bool exact_start = c0 == 0 || s0 == 0;
   const bool had = exact_start && p.has_prev[0] != 0;
   EmaState st{had ? p.prev[b] : 0.0, had && p.has_prev[1] != 0};
-  bool have = had;
+  bool use = smooth && had;  // this frame takes the EMA (no previous value: the raw value)
   // the row stride in a VGPR (opaque): the per-frame offsets are then vector arithmetic, instead of
   // 32 + 32 uniform 64-bit offsets the compiler would hold in (spilled) SGPRs
   int nb = p.nb;
@@ -310,8 +318,10 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
   // blocks of kEmaBlock frames from s0: c0 - s0 is a multiple of the block (kEmaWarm and kEmaChunk
   // are), so a block is all warm-up or all output. Loads are never guarded: band_raw and frame64 have
   // kEmaBlock spare rows past the last frame (values never used); only the stream's last partial
-  // block guards its stores.
+  // block guards its stores. A block's dtype flags come as one load per lane (lane l: frame f0 + l %
+  // kEmaBlock) and a ballot: bit i of `dm` = frame f0 + i holds a float64 array (uniform).
   float nx[kEmaBlock];
+  int nd;
   auto load = [&](int64_t g0) {
     const float* c = p.band_raw + g0 * nb + b;
 #pragma unroll
@@ -319,40 +329,121 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
       nx[i] = *c;
       c += nb;
     }
+    nd = p.frame64[g0 + (threadIdx.x & (kEmaBlock - 1))];
   };
   load(s0);
   for (int64_t f0 = s0; f0 < c1; f0 += kEmaBlock) {
     float x[kEmaBlock];
 #pragma unroll
     for (int i = 0; i < kEmaBlock; ++i) x[i] = nx[i];
+    const unsigned dm = (unsigned)__ballot(nd != 0);
     if (f0 + kEmaBlock < c1) load(f0 + kEmaBlock);
+    const int sf64 = __builtin_amdgcn_readfirstlane((int)st.f64);
     const int nf = c1 - f0 < kEmaBlock ? (int)(c1 - f0) : kEmaBlock;
     double v[kEmaBlock];
-#pragma unroll
-    for (int i = 0; i < kEmaBlock; ++i) {
-      const bool x64 = p.frame64[f0 + i] != 0;
-      v[i] = (smooth && have) ? ema_step(st, x[i], x64, k) : (double)x[i];
-      if (i < nf) st = EmaState{v[i], x64};
-      have = true;
-    }
-    if (f0 >= c0) {  // this chunk's frames (the warm-up frames belong to the chunk before)
-      double* o = p.band_out + f0 * nb + b;
+    if (use && dm == 0xFFFFFFFFu && sf64) {  // float64 arrays throughout: a = P f, b = x (1 - f) in float64
+      double w = st.v;
 #pragma unroll
       for (int i = 0; i < kEmaBlock; ++i) {
-        if (i < nf) *o = v[i];
-        o += nb;
+        w = w * k.f + (double)x[i] * k.g;
+        v[i] = w;
       }
+      st = EmaState{w, true};
+    } else if (use && dm == 0u && !sf64) {  // float32 arrays throughout
+      float w = (float)st.v;
+#pragma unroll
+      for (int i = 0; i < kEmaBlock; ++i) {
+        w = w * k.f32 + x[i] * k.g32;
+        v[i] = (double)w;
+      }
+      st = EmaState{(double)w, false};
+    } else {
+#pragma unroll
+      for (int i = 0; i < kEmaBlock; ++i) {
+        const bool d = (dm >> i) & 1u;
+        const double e = ema_step(st, x[i], d, k);
+        v[i] = use ? e : (double)x[i];  // (a select: the step always runs)
+        st = EmaState{v[i], d};         // (past the stream's last frame: never stored)
+        use = smooth;
+      }
+    }
+    if (!live) continue;
+    if (f0 >= c0) {  // this chunk's frames (the warm-up frames belong to the chunks before)
+      double* o = p.band_out + f0 * nb + b;
+      if (nf == kEmaBlock) {
+#pragma unroll
+        for (int i = 0; i < kEmaBlock; ++i) o[i * (int64_t)nb] = v[i];
+      } else {  // (unrolled with a guard: a dynamic index would put v in scratch memory)
+#pragma unroll
+        for (int i = 0; i < kEmaBlock; ++i)
+          if (i < nf) o[i * (int64_t)nb] = v[i];
+      }
+      if (f0 + kEmaBlock >= c1) {  // the chunk's last value (a select chain: v stays in registers)
+        double last = v[0];
+#pragma unroll
+        for (int i = 1; i < kEmaBlock; ++i) last = i < nf ? v[i] : last;
+        p.ema_end[blockIdx.y * (int64_t)p.nb + b] = last;
+      }
+    } else if (f0 + kEmaBlock == c0) {  // the warm-up's value at the frame before this chunk
+      p.ema_pre[blockIdx.y * (int64_t)p.nb + b] = v[kEmaBlock - 1];
     }
   }
 }
 
-// One thread per band, after post_ema_kernel: the chunks in order, each one's first value checked
-// against the step from the true state (the end of the chunk before, after its own check); equal bits
-// mean the rest of the chunk is the sequential recurrence already (the same operations on the same
-// values), otherwise the chunk is re-run from the true state. Writes the stream state for the next
-// call. The common path waits on no load: each chunk's first raw value, flag and stored values are
-// loaded kFixAhead chunks ahead.
-constexpr int kFixAhead = 8;
+// One thread per band, after post_ema_kernel. By induction over the chunks: when chunk c's warm-up
+// value at frame c0 - 1 (ema_pre) equals the (already true) value there (ema_end of chunk c - 1),
+// chunk c holds the sequential values; otherwise it is re-run from that true value until a recomputed
+// value equals the stored one (from there on the stored values are the recurrence's again: usually a
+// few frames, as the two runs differ by an ulp that the decay drops). A re-run that does not meet the
+// stored values by the chunk's end rewrote that end, so the next chunk is checked against the new
+// value. The checks run in parallel first (post_ema_check_kernel: one flag byte per chunk), then one
+// thread per band re-runs the flagged chunks in order (rare; kFixRun frames loaded at a time) and
+// writes the stream state for the next call.
+constexpr int kFixRun = 8;
+
+__global__ __launch_bounds__(64) void post_ema_check_kernel(PostParams p) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  const int64_t ch = blockIdx.y;
+  if (b >= p.nb) return;
+  const int64_t nch = (p.n + kEmaChunk - 1) / kEmaChunk, nchp = (nch + 15) / 16 * 16;
+  bool bad = false;
+  // (chunks whose warm-up starts at frame 0 continue the stream exactly)
+  if (ch > kEmaWarm / kEmaChunk && ch < nch)
+    bad = __double_as_longlong(p.ema_pre[ch * p.nb + b]) != __double_as_longlong(p.ema_end[(ch - 1) * p.nb + b]);
+  p.ema_flag[b * nchp + ch] = bad ? 1 : 0;
+}
+
+// re-run chunk frames [f0, f1] from the true value tv (dtype d64) at f0 - 1 until a recomputed value
+// equals the stored one; returns whether it met them (else *last = the rewritten value at f1)
+__device__ __forceinline__ bool ema_rerun(const PostParams& p, int b, int64_t f0, int64_t f1, double tv, bool d64,
+                                       const EmaCoef& k, double* last) {
+  const int64_t nb = p.nb;
+  EmaState st{tv, d64};
+  for (int64_t f = f0; f <= f1; f += kFixRun) {
+    float xr[kFixRun];
+    int dr[kFixRun];
+    double vr[kFixRun];
+#pragma unroll
+    for (int i = 0; i < kFixRun; ++i) {
+      const int64_t g = f + i <= f1 ? f + i : f1;
+      xr[i] = p.band_raw[g * nb + b];
+      dr[i] = p.frame64[g];
+      vr[i] = p.band_out[g * nb + b];
+    }
+#pragma unroll
+    for (int i = 0; i < kFixRun; ++i) {
+      if (f + i > f1) break;
+      const bool x64 = dr[i] != 0;
+      const double w = ema_step(st, xr[i], x64, k);
+      if (__double_as_longlong(w) == __double_as_longlong(vr[i])) return true;  // the stored run continues
+      p.band_out[(f + i) * nb + b] = w;
+      st = EmaState{w, x64};
+    }
+  }
+  *last = st.v;
+  return false;
+}
+
 __global__ __launch_bounds__(64) void post_ema_fix_kernel(PostParams p) {
   const int b = blockIdx.x * 64 + threadIdx.x;
   if (b >= p.nb) return;
@@ -360,53 +451,67 @@ __global__ __launch_bounds__(64) void post_ema_fix_kernel(PostParams p) {
   const bool smooth = (p.flags & 8) != 0;
   const int64_t n = p.n, nb = p.nb;
   const int64_t nch = (n + kEmaChunk - 1) / kEmaChunk;
-  auto last_of = [&](int64_t ch) { return (ch + 1) * kEmaChunk < n ? (ch + 1) * kEmaChunk - 1 : n - 1; };
-  int64_t e0 = last_of(0);
-  EmaState st{p.band_out[e0 * nb + b], p.frame64[e0] != 0};
+  OMEGA_STAMP(10);
+  int reruns = 0;
   if (smooth) {
-    for (int64_t ch0 = 1; ch0 < nch; ch0 += kFixAhead) {
-      float x0[kFixAhead];
-      double v0[kFixAhead], ve[kFixAhead];
-      bool d0[kFixAhead], de[kFixAhead];
+    bool dirty = false;  // the chunk before was re-run without meeting its stored values; its true
+    double carry = 0.0;  // last value is `carry`
+    // chunks whose warm-up starts at frame 0 continue the stream exactly: the checks start after them
+    for (int64_t g0 = kEmaWarm / kEmaChunk + 1; g0 < nch; g0 += 64) {
+      const int gn = nch - g0 < 64 ? (int)(nch - g0) : 64;
+      // the group's flag bytes (16 per load) -> one bit per chunk
+      const int64_t nchp = (nch + 15) / 16 * 16;
+      const uint4* fl = reinterpret_cast<const uint4*>(p.ema_flag + b * nchp + (g0 - g0 % 16));
+      const int sh = (int)(g0 % 16);  // (g0 - sh is a multiple of 16; the bits are shifted into place)
+      uint4 q[5];
 #pragma unroll
-      for (int j = 0; j < kFixAhead; ++j) {
-        const int64_t ch = ch0 + j < nch ? ch0 + j : nch - 1;
-        const int64_t f = ch * kEmaChunk, e = last_of(ch);
-        x0[j] = p.band_raw[f * nb + b];
-        d0[j] = p.frame64[f] != 0;
-        v0[j] = p.band_out[f * nb + b];
-        ve[j] = p.band_out[e * nb + b];
-        de[j] = p.frame64[e] != 0;
+      for (int j = 0; j < 5; ++j) q[j] = (g0 - sh + 16 * j < nchp) ? fl[j] : make_uint4(0, 0, 0, 0);
+      unsigned long long m80[2] = {0, 0};  // bits of chunks g0 - sh .. g0 - sh + 79
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        const unsigned w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const int bit = 16 * j + t;
+          if ((w[t / 4] >> (8 * (t % 4))) & 0xFFu) m80[bit / 64] |= 1ull << (bit % 64);
+        }
       }
-#pragma unroll
-      for (int j = 0; j < kFixAhead; ++j) {
-        const int64_t ch = ch0 + j;
-        if (ch >= nch) break;
-        const double v = ema_step(st, x0[j], d0[j], k);
-        if (__double_as_longlong(v) == __double_as_longlong(v0[j])) {
-          st = EmaState{ve[j], de[j]};
-          continue;
+      unsigned long long mm = sh ? (m80[0] >> sh) | (m80[1] << (64 - sh)) : m80[0];
+      if (gn < 64) mm &= (1ull << gn) - 1;
+      OMEGA_STAMP(11 + g0 / 64);
+      int c = -1;  // chunk g0 + c was the last one handled
+      while (true) {
+        double tv;
+        if (!dirty) {
+          if (!mm) break;
+          c = __ffsll((long long)mm) - 1;
+          mm &= mm - 1;
+          tv = p.ema_end[(g0 + c - 1) * nb + b];
+        } else {
+          if (++c >= gn) break;  // (the carry reaches the next group's first chunk)
+          mm &= ~(1ull << c);
+          if (__double_as_longlong(p.ema_pre[(g0 + c) * nb + b]) == __double_as_longlong(carry)) {
+            dirty = false;
+            continue;
+          }
+          tv = carry;
         }
-        // re-run this chunk from the true state (its later chunks' checks use the values written here)
-        const int64_t f1 = last_of(ch);
-        int64_t f = ch * kEmaChunk;
-        p.band_out[f * nb + b] = v;
-        st = EmaState{v, d0[j]};
-        for (++f; f <= f1; ++f) {
-          const bool x64 = p.frame64[f] != 0;
-          const double w = ema_step(st, p.band_raw[f * nb + b], x64, k);
-          p.band_out[f * nb + b] = w;
-          st = EmaState{w, x64};
-        }
+        ++reruns;
+        const int64_t f0 = (g0 + c) * kEmaChunk;
+        const int64_t f1 = f0 + kEmaChunk - 1 < n - 1 ? f0 + kEmaChunk - 1 : n - 1;
+        dirty = !ema_rerun(p, b, f0, f1, tv, p.frame64[f0 - 1] != 0, k, &carry);
       }
     }
-  } else {
-    st = EmaState{p.band_out[(n - 1) * nb + b], p.frame64[n - 1] != 0};
   }
-  p.prev_out[b] = st.v;
+  OMEGA_STAMP(20);
+  OMEGA_STAMP_AT(21, (unsigned long long)__popcll(__ballot(reruns >= 1)));
+  OMEGA_STAMP_AT(22, (unsigned long long)__popcll(__ballot(reruns >= 2)));
+  OMEGA_STAMP_AT(23, (unsigned long long)__popcll(__ballot(reruns >= 4)));
+  (void)reruns;
+  p.prev_out[b] = p.band_out[(n - 1) * nb + b];
   if (b == 0) {
     p.has_prev_out[0] = 1;
-    p.has_prev_out[1] = st.f64 ? 1 : 0;
+    p.has_prev_out[1] = p.frame64[n - 1] != 0 ? 1 : 0;
   }
 }
 
@@ -419,6 +524,8 @@ hipError_t launch_post(const PostParams& p, hipStream_t s) {
   if (p.nb > 0) {
     hipLaunchKernelGGL(post_ema_kernel, dim3((p.nb + 63) / 64, (unsigned)((p.n + kEmaChunk - 1) / kEmaChunk)), dim3(64), 0,
                        s, p);
+    hipLaunchKernelGGL(post_ema_check_kernel, dim3((p.nb + 63) / 64, (unsigned)((p.n + kEmaChunk - 1) / kEmaChunk)),
+                       dim3(64), 0, s, p);
     hipLaunchKernelGGL(post_ema_fix_kernel, dim3((p.nb + 63) / 64), dim3(64), 0, s, p);
   }
   return hipGetLastError();

@@ -60,5 +60,8 @@
 #define OMEGA_STAMP_RT(slot) \
   do {                       \
   } while (0)
+#define OMEGA_STAMP_AT(slot, clk) \
+  do {                            \
+  } while (0)
 #define OMEGA_STAMPS_GETTER(name)
 #endif
