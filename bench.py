@@ -160,19 +160,26 @@ class DeviceBackend:
         torch.cuda.synchronize(self.dev)
 
 
-def measure(be, rank, world, frames, steps, warmup, gather, seed_base=None):
+def prepare(be, rank, world, frames, seed_base=None):
+    """The inputs and output buffers of one measurement, made ahead of it (see main: no GPU idle between
+    the cfg4 line and the headline)."""
+    from omega_gpu import dist as D
+    sb = 2 * rank if seed_base is None else seed_base
+    x = be.input(frames, sb, sb + 1)
+    lay = D.PackedLayout(frames * C, T)
+    bufs = [be.alloc(lay) for _ in range(2)]
+    recv = [[be.alloc(lay) for _ in range(world)] if rank == 0 else None for _ in range(2)]
+    return x, lay, bufs, recv
+
+
+def measure(be, rank, world, frames, steps, warmup, gather, seed_base=None, prep=None):
     """Time `steps` passes of the hot path over this rank's batch of `frames` stereo frames (after
     `warmup` untimed ones), each step's packed outputs gathered to rank 0 asynchronously
     (double-buffered: step i waits only for the gather of step i - 2). Returns (max-over-ranks
     seconds, rank 0's last gathered blocks or None, layout)."""
     from omega_gpu import dist as D
-    sb = 2 * rank if seed_base is None else seed_base
-    x = be.input(frames, sb, sb + 1)
-    ncf = frames * C
-    lay = D.PackedLayout(ncf, T)
-    bufs = [be.alloc(lay) for _ in range(2)]
+    x, lay, bufs, recv = prep if prep is not None else prepare(be, rank, world, frames, seed_base)
     views = [lay.views(b) for b in bufs]
-    recv = [[be.alloc(lay) for _ in range(world)] if rank == 0 else None for _ in range(2)]
     pending = [None, None]
     be.reset()
 
@@ -638,16 +645,35 @@ def main(argv=None):
     gather = world > 1 and not a.no_gather
 
     frames = a.frames
-    dt, got, lay = measure(be, rank, world, frames, a.steps, a.warmup, gather)
+    prep_main = prepare(be, rank, world, frames) if not standin else None
+    # The cfg4 line (every rank: the per-GPU shard, ~25 ms of the same path) runs right before the
+    # headline, its inputs and the headline's made beforehand so the GPU does not idle in between:
+    # MI355X lowers its clock after a few ms of idle and takes ~30 ms of load to raise it again
+    # (tools/ramp_probe.py: 89.8 us per step in the first 20 steps out of idle, 79.7 after 350; after
+    # a 5 ms pause 90.0 again; after 25 cfg4 steps instead of the pause 79.9 -- DESIGN.md §5), so the
+    # headline's K steps are timed at the clock the path runs at in continuous service.
+    cfg4 = None
+    if not standin and not a.no_cfg4:
+        dt4, _, _ = measure(be, rank, world, FRAMES_CFG4, a.cfg4_steps, 3, gather)
+        ncf4 = FRAMES_CFG4 * C
+        cfg4 = {"workload": f"cfg4 per-GPU shard: {FRAMES_CFG4} stereo frames x 16384 per GPU "
+                            f"({FRAMES_CFG4 * world} stereo frames over {world} GPU(s); BASELINE cfg4 = 32768 "
+                            "over 8), same per-step path as the headline line" +
+                            (", packed outputs gathered to rank 0 over RCCL each step" if gather else "") +
+                            "; measured first, out of idle (its steps include the clock ramp)",
+                "value": ncf4 * world * a.cfg4_steps / dt4, "unit": "channel-frames/s",
+                "ms_per_step": dt4 / a.cfg4_steps * 1e3, "steps": a.cfg4_steps,
+                "channel_frames_per_gpu": ncf4, "global_stereo_frames": FRAMES_CFG4 * world}
+    dt, got, lay = measure(be, rank, world, frames, a.steps, a.warmup, gather, prep=prep_main)
     ncf = frames * C
     value = ncf * world * a.steps / dt
     if a.dump and rank == 0 and got is not None:
         np.save(a.dump, torch.stack([g.cpu() for g in got]).numpy())
 
     roof = None
-    cfg4 = None
     if not standin:
-        kt_ms, kcf = kernel_time_ms(be.eng, be.input(frames, 2 * rank, 2 * rank + 1))
+        # (right after the headline, on its input: no idle in between, see above)
+        kt_ms, kcf = kernel_time_ms(be.eng, prep_main[0])
         flop_launch = (FLOP_FFT + FLOP_KW + FLOP_TP) * kcf
         achieved = flop_launch / (kt_ms * 1e-3) / 1e12
         traffic, traffic_src = kernel_traffic("batch")
@@ -663,16 +689,6 @@ def main(argv=None):
                         "channel-frame = SURVEY.md §8(d) FFT 1.09 M + KW 0.67 M + TP 3.33 M (the reference's "
                         "resample algorithm); kernel_ms = HIP-event average of 20 back-to-back launches on the "
                         "launch stream"}
-        if not a.no_cfg4:
-            dt4, _, _ = measure(be, rank, world, FRAMES_CFG4, a.cfg4_steps, 3, gather)
-            ncf4 = FRAMES_CFG4 * C
-            cfg4 = {"workload": f"cfg4 per-GPU shard: {FRAMES_CFG4} stereo frames x 16384 per GPU "
-                                f"({FRAMES_CFG4 * world} stereo frames over {world} GPU(s); BASELINE cfg4 = 32768 "
-                                "over 8), same per-step path as the headline line" +
-                                (", packed outputs gathered to rank 0 over RCCL each step" if gather else ""),
-                    "value": ncf4 * world * a.cfg4_steps / dt4, "unit": "channel-frames/s",
-                    "ms_per_step": dt4 / a.cfg4_steps * 1e3, "steps": a.cfg4_steps,
-                    "channel_frames_per_gpu": ncf4, "global_stereo_frames": FRAMES_CFG4 * world}
     cfg5 = None
     if not standin and not a.no_cfg5:
         cfg5 = cfg5_line(rank, world, be.dev, a.cfg5_seconds)

@@ -21,7 +21,11 @@ def main():
     ap.add_argument("stage")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--frames", type=int, default=256, help="stereo frames per call (cfg2: 256, cfg4 shard: 4096)")
+    ap.add_argument("--lib", default=None, help="another build in lib/ (A/B of two builds on one box)")
     a = ap.parse_args()
+    if a.lib:
+        from omega_gpu import _lib as L0
+        L0.use_development_library(a.lib)
     import bench
     from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
     from omega_gpu import _lib as L
