@@ -8,9 +8,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/round
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python bench.py > $OUT/bench.json
+# the driver's command, then the same under rocprofv3 (no CPU baseline: host-only work)
+timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json
 cat $OUT/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --steps 50 --warmup 5 --no-cpu-baseline > $OUT/stats.json 2> $OUT/stats.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/stats.json 2> $OUT/stats.log
 for stage in batch spectra; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_${stage}_$c -o run -- python tools/kernel_bench.py $stage --reps 20 > $OUT/pmc_${stage}_$c.log 2>&1

@@ -2,7 +2,8 @@
 """Turn gpurun_out/round (tools/profile_round.sh) into the committed evidence under profiles/:
 
   rNN_bench.json              the bench line of that run
-  rNN_bench_kernel_stats.csv  rocprofv3 --kernel-trace --stats of `bench.py --steps 50 --warmup 5`
+  rNN_bench_kernel_stats.csv  rocprofv3 --kernel-trace --stats of the driver's bench command
+                              (`bench.py --gpus 1 --steps 20 --warmup 5`, without the CPU baseline)
   rNN_bench_dispatches.md     per-kernel dispatch averages; the true-peak dispatches split into the
                               in-pipeline ones (overlapped with the other streams) and the roofline
                               probe's back-to-back ones (what bench.py's roofline.kernel_ms times)
@@ -39,18 +40,20 @@ def main(rnd):
     per = {}
     for r in rows:
         per.setdefault(short(r["Kernel_Name"]), []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    lines = [f"# Round {rnd}: kernel dispatches of `python bench.py --steps 50 --warmup 5 --no-cpu-baseline`",
+    lines = [f"# Round {rnd}: kernel dispatches of `python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline`",
              "", "Source: rocprofv3 --kernel-trace --stats (r%s_bench_kernel_stats.csv); durations in us." % rnd, "",
              "| kernel | dispatches | avg | min | max |", "|---|---|---|---|---|"]
     for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
         lines.append(f"| `{k}` | {len(v)} | {sum(v) / len(v):.1f} | {min(v):.1f} | {max(v):.1f} |")
-    # batch_kernel dispatches by grid: the cfg2 step's launch (512 channel-frames) comes first in bench.py --
-    # 55 pipeline steps (5 warmup + 50 timed), then the roofline probe's 3 + 20 back-to-back launches without
-    # the meter kernels beside it; cfg4 (8192 channel-frames per launch) and the cfg5 stream use other grids
+    # batch_kernel dispatches by grid: the cfg2 step's launch (512 channel-frames, the most frequent grid) --
+    # 25 pipeline steps (5 warmup + 20 timed, after the cfg4 line's 8192-channel-frame launches), then the
+    # roofline probe's 3 + 20 back-to-back launches without the meter kernels beside it; the cfg5 stream
+    # uses other grids
     bk = [r for r in rows if short(r["Kernel_Name"]) == TP]
-    steps = 55
+    steps = 25
     if bk:
-        g0 = bk[0]["Grid_Size_X"]
+        grids = [r["Grid_Size_X"] for r in bk]
+        g0 = max(set(grids), key=grids.count)
         cfg2 = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in bk if r["Grid_Size_X"] == g0]
         pipe, timed = cfg2[:steps], cfg2[steps + 3:steps + 23]
         lines += ["", f"Batch kernel `{TP}` (all per-channel-frame work of a step in one launch), cfg2 grid {g0}:", "",
