@@ -945,6 +945,24 @@ def test_app_post_ema_slow_factors_exact():
     np.testing.assert_array_equal(b, wb)
 
 
+def test_app_post_ema_chunk_groups_exact():
+    """One 5000-frame call (79 EMA chunks: the boundary checks and re-runs go in groups of 64 chunks)
+    with a 800-frame silence across the group boundary at frame 4096, where the decaying bands make
+    every warmed-up chunk re-run and the rewritten chunk ends carry into the next group: equal bit for
+    bit to the same frames in single-frame calls (each one the plain sequential step, golden-tested)."""
+    from omega_gpu.app_post import SpectrumPostProcessor
+    freqs = load_golden("app_post")["default/freqs"]
+    rng = np.random.default_rng(23)
+    x = (rng.random((5000, 512)) * rng.random((5000, 1)) ** 2).astype(np.float32)
+    x[3800:4600] = 0.0
+    pp = SpectrumPostProcessor(freqs)
+    _, b, c = pp.process(x)
+    pp.reset()
+    seq = np.concatenate([pp.process(x[f:f + 1])[1] for f in range(len(x))])
+    np.testing.assert_array_equal(b, seq)
+    assert (b[4599] > 0).sum() > 100  # (still decaying at the end of the silence)
+
+
 def test_app_post_content_threshold_frames():
     """Frames whose bass ratio sits within a few ulps of the 0.6 threshold, where float64 range sums
     and numpy's float32 pairwise np.mean disagree (tests/golden/gen_post_threshold.py): the device
