@@ -29,7 +29,7 @@ hipError_t launch_mrfft(const SpectralParams& p, hipStream_t s);
 hipError_t launch_mrfft_range(const SpectralParams& p, int r0, int r1, hipStream_t s);
 hipError_t launch_mrfft_independent(const SpectralParams& p, hipStream_t s);
 hipError_t launch_truepeak(int W, const SpectralParams& p, hipStream_t s);
-hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s);
+hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s, int extra_lds = 0);
 hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s);
 hipError_t launch_rfft(int m, const RfftParams& p, hipStream_t s);
 hipError_t launch_kweight(int m, const KWeightParams& p, hipStream_t s);
@@ -960,7 +960,8 @@ const char* omega_version(void) { return "omega-mi355x 0.1 (gfx950, ABI 1)"; }
 // Development build only (make dev): one kernel variant over n_cf channel-frames of the context's
 // frames x (device memory, frame stride W, channel stride W * ... as omega_process_frames with
 // frame_stride = C * W, channel_stride = W), outputs to device buffers. which: 0 the 16384-point
-// resolution kernel, 2 the true-peak kernel (aux: [n_cf] true peaks). (Two frames per workgroup
+// resolution kernel, 2 the true-peak kernel (aux: [n_cf] true peaks), 3 the same at one workgroup per
+// CU (dynamic LDS padded past half the CU's 160 KiB). (Two frames per workgroup
 // through one exchange buffer -- the 16384-point resolution interleaved, and a true peak with its
 // spectrum parked in L2 between phases -- measured no faster at 8192 channel-frames (true peak 614 vs
 // 621 us at a shader clock of 1773 vs 1897 MHz): the extra frames in flight bought activity and the
@@ -982,6 +983,8 @@ int omega_dev_probe(omega_ctx* c, int which, const float* x, int64_t n_frames, f
   sp.rot = rot;
   if (which == 0) e = launch_mrfft_rf(16384, sp, 0, c->stream);
   if (which == 2) e = launch_truepeak_rf(16384, sp, c->stream);
+  // 3: the true-peak kernel at one workgroup per CU (extra dynamic LDS), the occupancy probe
+  if (which == 3) e = launch_truepeak_rf(16384, sp, c->stream, 16 * 1024);
   return e == hipSuccess ? 0 : fail(c, OMEGA_EHIP, "probe %d: %s", which, hipGetErrorString(e));
 }
 #endif

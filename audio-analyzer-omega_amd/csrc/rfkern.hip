@@ -553,10 +553,12 @@ hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s) {
+// extra_lds: dynamic LDS past what the kernel uses (the development probe's occupancy sweep: 0 in the
+// product)
+hipError_t launch_truepeak_rf(int W, const SpectralParams& p, hipStream_t s, int extra_lds) {
   const dim3 grid((unsigned)p.n_cf);
   if (W == 16384) {
-    hipLaunchKernelGGL(truepeak_rf_kernel<8192>, grid, dim3(512), lds_bytes<8192>(), s, p);
+    hipLaunchKernelGGL(truepeak_rf_kernel<8192>, grid, dim3(512), lds_bytes<8192>() + extra_lds, s, p);
   } else if (W == 8192) {
     hipLaunchKernelGGL(truepeak_rf_kernel<4096>, grid, dim3(256), lds_bytes<4096>(), s, p);
   } else {
