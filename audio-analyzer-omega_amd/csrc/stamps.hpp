@@ -3,6 +3,11 @@
 // at numbered points; OMEGA_STAMP_RT(slot) records s_memrealtime (the device-wide 100 MHz clock);
 // tools/stamps.py reads them. Compiled out of the product library.
 #pragma once
+// OMEGA_WGTRACE alone: only the whole-grid workgroup trace (no phase stamps), for a build whose
+// register allocation stays the product's (make trace -> lib/libomega_trace.so)
+#if defined(OMEGA_WGTRACE) && !defined(OMEGA_STAMPS)
+#define OMEGA_WGTRACE_ONLY 1
+#endif
 #ifdef OMEGA_STAMPS
 #define OMEGA_STAMPS_DECL static __device__ unsigned long long g_stamps[8 * 16 * 32];
 #define OMEGA_STAMP_ROW() \
@@ -22,6 +27,40 @@
 // Whole-grid workgroup trace: per workgroup {s_memrealtime at entry, at exit, role, HW_ID | XCC_ID
 // << 32, s_memtime at entry, at exit} (the shader clock over the 100 MHz real-time clock gives the
 // clock the workgroup ran at), read by tools/wgtrace.py.
+#define OMEGA_WGTRACE_CAP 65536
+#define OMEGA_WGTRACE_DECL static __device__ unsigned long long g_wgtrace[OMEGA_WGTRACE_CAP * 6];
+#define OMEGA_WG_BEGIN()                                                                       \
+  const unsigned long long wg_t0_ = __builtin_amdgcn_s_memrealtime();                         \
+  const unsigned long long wg_c0_ = __builtin_amdgcn_s_memtime()
+#define OMEGA_WG_END(role)                                                                     \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < OMEGA_WGTRACE_CAP) {                                  \
+      unsigned long long* q_ = g_wgtrace + 6 * (size_t)blockIdx.x;                             \
+      q_[5] = __builtin_amdgcn_s_memtime();                                                    \
+      q_[1] = __builtin_amdgcn_s_memrealtime();                                                \
+      q_[0] = wg_t0_;                                                                          \
+      q_[4] = wg_c0_;                                                                          \
+      q_[2] = (unsigned long long)(role);                                                      \
+      q_[3] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                  \
+              ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);          \
+    }                                                                                          \
+  } while (0)
+#define OMEGA_WGTRACE_GETTER(name)                                                             \
+  extern "C" int name(unsigned long long* host) {                                              \
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wgtrace), sizeof(g_wgtrace));          \
+  }
+#elif defined(OMEGA_WGTRACE_ONLY)
+#define OMEGA_STAMPS_DECL
+#define OMEGA_STAMP(slot) \
+  do {                    \
+  } while (0)
+#define OMEGA_STAMP_RT(slot) \
+  do {                       \
+  } while (0)
+#define OMEGA_STAMP_AT(slot, clk) \
+  do {                            \
+  } while (0)
+#define OMEGA_STAMPS_GETTER(name)
 #define OMEGA_WGTRACE_CAP 65536
 #define OMEGA_WGTRACE_DECL static __device__ unsigned long long g_wgtrace[OMEGA_WGTRACE_CAP * 6];
 #define OMEGA_WG_BEGIN()                                                                       \

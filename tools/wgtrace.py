@@ -16,7 +16,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from omega_gpu import _lib as _L  # noqa: E402
 
-_L.use_development_library("libomega_dev.so")
+_L.use_development_library("libomega_trace.so" if "--trace" in sys.argv else "libomega_dev.so")
 
 ROLE = {0: "kw", 1: "tp", 2: "res16k", 20: "spectra", 3 + 512: "res512", 3 + 1024: "res1k", 3 + 2048: "res2k",
         3 + 4096: "res4k", 3 + 8192: "res8k"}
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--probe", type=int, default=None, help="trace omega_dev_probe(which) instead of the batch")
     ap.add_argument("--cfg3", action="store_true", help="trace the cfg3 spectra kernel (4096 frames of 8192)")
+    ap.add_argument("--trace", action="store_true", help="the trace-only build (make trace): product registers")
     a = ap.parse_args()
     import bench
     from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
@@ -92,6 +93,23 @@ def main():
     full = 2 * ncu
     busy = np.sum(end - beg)
     print(f"  slot-time used {busy:.0f} WG-us of {full * span:.0f} ({busy / (full * span) * 100:.1f} % of 2 slots/CU x span)")
+    # hand-off gaps: on each CU, from a workgroup's end marker to the next workgroup's begin marker
+    # (the next one to start after that end, in the first 90 % of the span: launch + first-instruction
+    # latency + the ended workgroup's remaining waves)
+    gaps = []
+    for cu in np.unique(cu_key):
+        sel = cu_key == cu
+        b_cu, e_cu = np.sort(beg[sel]), np.sort(end[sel])
+        for e in e_cu:
+            if e > 0.9 * span:
+                continue
+            j = np.searchsorted(b_cu, e)
+            if j < len(b_cu):
+                gaps.append(b_cu[j] - e)
+    if gaps:
+        g = np.array(gaps)
+        print(f"  hand-off gaps (us): p10 {np.percentile(g, 10):.2f}  p50 {np.median(g):.2f}  p90 "
+              f"{np.percentile(g, 90):.2f}  mean {g.mean():.2f}  over {len(g)} workgroup ends")
     first_drop = next((b for b, v in zip(bins, res) if b > 5 and v < 0.9 * full), None)
     print(f"  ramp: {next((b for b, v in zip(bins, res) if v >= 0.95 * full), None)} us to 95 % residency; "
           f"residency below 90 % from {first_drop} us to the end ({span:.1f})")
