@@ -49,7 +49,8 @@ hipError_t launch_vu(const VuParams& p, hipStream_t s);
 hipError_t launch_transients(const TransientParams& p, hipStream_t s);
 hipError_t launch_transients_any(const TransientParams& p, hipStream_t s);
 hipError_t launch_post(const PostParams& p, hipStream_t s);
-hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s);
+hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, const MeterPrepParams& mp,
+                        int grid, hipStream_t s);
 }  // namespace omega
 
 using namespace omega;
@@ -58,6 +59,7 @@ namespace {
 
 constexpr double kPi = 3.14159265358979323846;
 constexpr int kChunkFrames = kMeterChunk;
+constexpr int kBatchWaves = 8;  // waves of a batch_kernel workgroup (rfkern.hip kBatchThreads / 64)
 
 struct DevBuf {
   void* p = nullptr;
@@ -216,6 +218,8 @@ struct omega_ctx {
   unsigned* d_kw_done = nullptr;  // batch_kernel's K-weighting workgroups count themselves in here
   unsigned kw_issued = 0;         // K-weighting workgroups launched with the count on (wraps)
   unsigned q_issued = 0;          // LUFS-meter query workgroups launched with the count on (d_kw_done[1])
+  unsigned tp_issued = 0;         // batch true-peak workgroups launched with the count on (d_kw_done[2])
+  unsigned prep_issued = 0;       // meter prep workgroups launched with the count on (d_kw_done[3])
   // device-side poll expiry flags (host-mapped: [0] meter prep, [1] join), checked by
   // check_device_err; the poll bound (OMEGA_POLL_LIMIT, a test knob)
   unsigned* h_err = nullptr;
@@ -674,7 +678,7 @@ int build_meter_state(omega_ctx* c) {
     HIPC(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_err), c->h_err, 0));
   }
   HIPC(c, hipMemset(c->d_kw_done, 0, 8 * sizeof(unsigned)));
-  c->kw_issued = c->q_issued = 0;
+  c->kw_issued = c->q_issued = c->tp_issued = c->prep_issued = 0;
   return omega_meter_reset(c);
 }
 
@@ -829,17 +833,22 @@ bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams&
 }
 
 // The default layout for 16384-sample frames. On `s`: one batch_kernel launch (BatchPlan: K-weighting
-// and 16384-point-resolution workgroups mixed, then the true peaks, then the small resolutions) and the
-// true-peak meter. On fork[0]: the meter prep (it waits on the K-weighting count, kw_done) and the LUFS
-// meters (their workgroups count themselves in). The true-peak meter's first workgroup waits for that
-// count, so `s` completes only after fork[0]'s work: no stream events anywhere (each event record /
-// wait cost ~7-13 us of idle GPU between kernels). Mixing the latency-bound K-weighting scans with
+// and 16384-point-resolution workgroups mixed, then the true peaks, then the small resolutions, then --
+// for a batch of at most kChunkFrames frames per channel -- the meter aggregates as the grid's last
+// segment). On fork[0]: the meter prep (it waits on the K-weighting count, kw_done, and counts itself
+// in). The meter workgroups wait for the prep's count and for the true peaks' count, so `s` completes
+// only after fork[0]'s work: no stream events and no kernel after the batch (each event record / wait
+// cost ~7-13 us of idle GPU between kernels). Longer batches (chunks chained through the per-context
+// scratch) keep the meter query kernels: the LUFS query on fork[0] counting itself in, the true-peak
+// query after the batch on `s` joining that count. Mixing the latency-bound K-weighting scans with
 // transform work is what pays (K-weighting alone 25.7 us, the true peak 37, the resolutions 26.5; one
-// batch launch of all three 73.9). Measured and rejected on MI355X (round 1-2): other role
+// batch launch of all three 73.9). Measured and rejected on MI355X (rounds 1-3): other role
 // orders (K-weighting as its own kernel 110.4 us per step; mixed with the true peaks 85.2; the true
-// peaks first ~equal), the meter queries after the batch (88 vs 81-82), the true-peak query on the side
-// stream joined in the batch's last workgroup (85-87), the true-peak meter as a batch role (86-88), the
-// true-peak meter by the batch's last true-peak workgroup, joined there (86.2 vs 81.1, round 3).
+// peaks first ~equal; role chunks of one workgroup per CU), the meter queries after the batch (88 vs
+// 81-82), the true-peak query on the side stream joined in the batch's last workgroup (85-87), the
+// true-peak meter as a batch role (86-88), the true-peak meter by the batch's last true-peak workgroup,
+// joined there (86.2 vs 81.1, round 3). The in-grid meter segment measured even with the query kernels
+// (step 79.4-80.6 vs 79.0-79.4 us) at two fewer launches per call (host enqueue 13-17 vs 22-27 us).
 int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
                   const float* tp, double* meters, hipStream_t s, int mr, bool do_tp, bool do_kw) {
   (void)W;
@@ -873,9 +882,43 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
     ++bp.multi.n_seg;
     nwg += (n + fpw - 1) / fpw;
   }
-  const int64_t grid = end + nwg;
+  // the meter aggregates of a one-chunk batch as the grid's last segment (batch_meter_role): the prep
+  // kernel on fork[0] (it waits for the K-weighting count) counts itself in, the true-peak workgroups
+  // count themselves in, the meter workgroups wait for both; longer batches chain their chunks through
+  // the per-context scratch and keep the query kernels
+  const bool in_grid = meters && do_tp && do_kw && n_frames > 0 && n_frames <= kChunkFrames;
+  const int64_t n_mq = in_grid ? (n + kBatchWaves - 1) / kBatchWaves : 0;
+  bp.q_begin = (int)(end + nwg);
+  bp.q_n = (int)n_mq;
+  const int64_t grid = end + nwg + n_mq;
   if (grid > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
+  MeterPrepParams mq{};
   std::vector<MeterPrepParams> mc;
+  if (in_grid) {
+    mc = meter_chunks(c, lufs, tp, n_frames, meters);
+    kp.kw_done = c->d_kw_done;
+    c->kw_issued += (unsigned)n;
+    MeterPrepParams p = mc[0];
+    p.wait_ctr = c->d_kw_done;
+    p.wait_target = c->kw_issued;
+    p.q_done = c->d_kw_done + 3;
+    HIPC(c, launch_meter_prep(p, c->fork[0]));
+    c->prep_issued += (unsigned)p.C;
+    mq = mc[0];
+    mq.start_ctr = c->d_kw_done + 3;
+    mq.start_target = c->prep_issued;
+    sp.tp_done = c->d_kw_done + 2;
+    mq.join_ctr = c->d_kw_done + 2;
+    mq.join_target = c->tp_issued + (unsigned)n;
+    const hipError_t le = launch_batch(sp, kp, bp, mq, (int)grid, s);
+    if (le != hipSuccess) {
+      // the prep kernel already waits for this batch's count: publish it (see below)
+      (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
+      return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
+    }
+    c->tp_issued += (unsigned)n;
+    return 0;
+  }
   if (meters) {
     mc = meter_chunks(c, lufs, tp, n_frames, meters);
     kp.kw_done = c->d_kw_done;
@@ -894,7 +937,7 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
     }
   }
   if (grid > 0) {
-    const hipError_t le = launch_batch(sp, kp, bp, (int)grid, s);
+    const hipError_t le = launch_batch(sp, kp, bp, mq, (int)grid, s);
     if (le != hipSuccess) {
       // the prep kernel already waits for this batch's count: publish it, so that it (and every later
       // call's target) stays in step with the device counter instead of timing out

@@ -23,12 +23,14 @@
 //     those) sits at merged rank j + its core count, so the k-th order statistic is either such an
 //     extra or core[k - #extras ranked below k] -- a pass over the extras, no per-frame sort.
 #include "fft.hpp"
+#include "meter_query.hpp"
 #include "params.hpp"
 #include "stamps.hpp"
 
 namespace omega {
 
 OMEGA_STAMPS_DECL
+OMEGA_MARKS_DECL
 
 constexpr int kNewCap = kMeterChunk;
 constexpr int kHistCap = kMeterHistCap;
@@ -135,12 +137,6 @@ __device__ __forceinline__ Scan4 block_excl_scan4(const Scan4& x, int* wsa, int*
   return Scan4{rl(sa) + ia - x.a, rl(sb) + ib - x.b, rl(sc) + ic - x.c, rld(sd) + id - x.d};
 }
 
-// Window of batch frame f as absolute frame indices [lo, hi] (hi = T0 + f).
-__device__ __forceinline__ uint32_t window_lo(uint32_t T0, int nh, int64_t f, int int_len) {
-  const int64_t n = nh + f + 1;
-  return T0 - (uint32_t)nh + (uint32_t)(n - min<int64_t>(int_len, n));
-}
-
 // The stream's LUFS_inst sequence over [T0 - nh, T0 + F) lives in LDS (V); every global input is
 // fetched once, up front.
 __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
@@ -156,6 +152,7 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   __shared__ double wsd[16];
   unsigned long long* K64 = reinterpret_cast<unsigned long long*>(kb);
   const int c = blockIdx.x, tid = threadIdx.x;
+  OMEGA_MARK(c, 0);
   if (p.wait_ctr) {
     // the batch's LUFS_inst values come from batch_kernel on another stream: one lane polls the count
     // (relaxed, bounded), then ONE agent-scope acquire before any wave reads them
@@ -175,6 +172,7 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     }
     __syncthreads();
   }
+  OMEGA_MARK(c, 1);
   const int C = p.C, F = (int)p.n_frames;
   const uint32_t T0 = p.t0_in[c];
   const int nh = p.n_l_in[c], ns = p.n_s_in[c];
@@ -407,6 +405,7 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   for (int i = tid; i < klen; i += 1024) p.hist_l_out[(int64_t)c * p.HL + i] = V[L - klen + i];
   if (tid == 0) p.n_l_out[c] = klen;
   OMEGA_STAMP(7);
+  OMEGA_MARK(c, 2);
   if (p.q_done) {
     // (tail layout) count this channel's prep in for the query kernel on the other stream: every
     // wave's stores drained, then one agent-scope release before the add
@@ -420,128 +419,16 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   }
 }
 
-__device__ __forceinline__ double lerp_pct(double a, double b, double gamma) {
-  const double d = b - a;  // numpy _lerp
-  return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
-}
-
-__device__ __forceinline__ float seq_at(const float* hist, const float* batch, int nh, int HC, int C, int c,
-                                        int64_t i) {
-  return i < nh ? hist[(int64_t)c * HC + i] : batch[(i - nh) * C + c];
-}
-
 // One wave per output (f, c); workgroup (0, c) also rolls the channel's true-peak history. parts
 // selects the LUFS meters (they need the prep kernel's output) and/or the true-peak meter (it needs the
 // batch's true peaks only), so the two can run on different streams.
 __device__ __forceinline__ void meter_query_body(const MeterPrepParams& p) {
-  const int lane = threadIdx.x & 63;
   const int c = blockIdx.y;
-  const int C = p.C;
-  const int nt = p.n_t_in[c];
-  const int64_t F = p.n_frames;
   const bool do_l = p.parts & 1, do_t = p.parts & 2;
-  if (blockIdx.x == 0 && do_t) {
-    const int64_t tt = (int64_t)nt + F;
-    const int ktl = (int)min<int64_t>(p.HT, tt);
-    for (int i = threadIdx.x; i < ktl; i += 256) {
-      const int64_t j = tt - ktl + i;
-      p.hist_t_out[(int64_t)c * p.HT + i] = j < nt ? p.hist_t_in[(int64_t)c * p.HT + j] : p.tp[(j - nt) * C + c];
-    }
-    if (threadIdx.x == 0) p.n_t_out[c] = ktl;
-  }
+  if (blockIdx.x == 0 && do_t) meter_roll_tp(p, c, threadIdx.x, 256);
   const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (f >= F) return;
-  if (do_t) {
-    const int64_t ntp = nt + f + 1, wt = min<int64_t>(p.peak_len, ntp);
-    float tpm = -INFINITY;
-    for (int64_t i = lane; i < wt; i += 64) tpm = fmaxf(tpm, seq_at(p.hist_t_in, p.tp, nt, p.HT, C, c, ntp - wt + i));
-    tpm = wave_max(tpm);
-    if (lane == 0) p.out[(f * C + c) * 5 + 4] = (double)tpm;
-  }
-  if (!do_l) return;
-  const int nh = p.n_l_in[c];
-  const uint32_t T0 = p.t0_in[c];
-  const int64_t n = nh + f + 1;  // the sequence known to this frame, local index 0 = absolute T0 - nh
-  double sm = 0.0, ss = 0.0;
-  const int64_t wm = min<int64_t>(p.mom_len, n), ws = min<int64_t>(p.short_len, n);
-  for (int64_t i = lane; i < ws; i += 64) {
-    const double v = seq_at(p.hist_l_in, p.lufs, nh, p.HL, C, c, n - ws + i);
-    ss += v;
-    if (i >= ws - wm) sm += v;
-  }
-  sm = wave_sum(sm);
-  ss = wave_sum(ss);
-  // integrated window: local [n - wi, n) = absolute [lo, hi]
-  const int64_t wi = min<int64_t>(p.int_len, n);
-  const int* gp = p.gcount + (int64_t)c * (kSeqCap + 1);
-  const double* gsum = p.gsum + (int64_t)c * (kSeqCap + 1);
-  const int ng = gp[n] - gp[n - wi];
-  double integ = -100.0, range = 0.0;
-  if (ng > 0) {
-    integ = (gsum[n] - gsum[n - wi]) / ng;
-    const uint32_t lo = window_lo(T0, nh, f, p.int_len), hi = T0 + (uint32_t)f;
-    const uint32_t clo = window_lo(T0, nh, F - 1, p.int_len), chi = T0;
-    const bool has_core = (int32_t)(chi - clo) >= 0;
-    int want[4];
-    double gam[2];
-    const double qs[2] = {0.10, 0.95};
-    for (int q = 0; q < 2; ++q) {
-      const double vi = (double)(ng - 1) * qs[q];
-      int prev = (int)floor(vi);
-      if (vi >= (double)(ng - 1)) prev = ng - 1;
-      want[2 * q] = prev;
-      want[2 * q + 1] = min(prev + 1, ng - 1);
-      gam[q] = vi - floor(vi);
-    }
-    // extras in value order, 64 per round; a member's merged rank is (members before it) + rc
-    const MeterExt* ext = p.ext + (int64_t)c * kSeqCap;
-    const int ne = p.n_ext[c];
-    float val[4] = {0.f, 0.f, 0.f, 0.f};
-    int below[4] = {0, 0, 0, 0};  // member extras of merged rank < want
-    bool found[4] = {false, false, false, false};
-    int jb = 0;
-    // kExtRounds rounds of 64 extras loaded together (one L2 latency per group instead of per round:
-    // the query runs beside the batch kernel, and its resident time costs the batch register slots)
-    constexpr int kExtRounds = 4;
-    for (int g0 = 0; g0 < ne; g0 += 64 * kExtRounds) {
-      MeterExt eg[kExtRounds];
-#pragma unroll
-      for (int q = 0; q < kExtRounds; ++q) {
-        const int i = g0 + 64 * q + lane;
-        eg[q] = i < ne ? ext[i] : MeterExt{0.f, 0u, 0, 0};
-      }
-#pragma unroll
-      for (int q = 0; q < kExtRounds; ++q) {
-        const MeterExt e = eg[q];
-        const bool mem = g0 + 64 * q + lane < ne && (uint32_t)(e.t - lo) <= hi - lo &&
-                         !(has_core && (uint32_t)(e.t - clo) <= chi - clo);
-        const unsigned long long bm = __ballot(mem);
-        const int rank = jb + __popcll(bm & ((1ull << lane) - 1ull)) + e.rc;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          below[w] += __popcll(__ballot(mem && rank < want[w]));
-          const unsigned long long hit = __ballot(mem && rank == want[w]);
-          if (hit) {
-            found[w] = true;
-            val[w] = __shfl(e.v, __ffsll((long long)hit) - 1, 64);
-          }
-        }
-        jb += __popcll(bm);
-      }
-    }
-    const float* core = p.core + (int64_t)c * kSeqCap;
-#pragma unroll
-    for (int w = 0; w < 4; ++w)
-      if (!found[w]) val[w] = core[want[w] - below[w]];
-    range = lerp_pct(val[2], val[3], gam[1]) - lerp_pct(val[0], val[1], gam[0]);
-  }
-  if (lane == 0) {
-    double* out = p.out + (f * C + c) * 5;
-    out[0] = sm / (double)wm;
-    out[1] = ss / (double)ws;
-    out[2] = integ;
-    out[3] = range;
-  }
+  if (f >= p.n_frames) return;
+  meter_query_wave(p, f, c, threadIdx.x & 63, do_l, do_t);
 }
 
 __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
@@ -591,6 +478,7 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
 }
 
 OMEGA_STAMPS_GETTER(omega_debug_meter_stamps)
+OMEGA_MARKS_GETTER(omega_debug_marks_meters)
 
 // prep needs the batch's LUFS_inst only; query also reads its true peaks
 hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s) {

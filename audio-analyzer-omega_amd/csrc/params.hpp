@@ -203,15 +203,20 @@ struct MultiPlan {
 // 16384-point resolution (mr_res). Two segments of role groups, then the small resolutions:
 //   [seg_begin[s], seg_begin[s + 1])  groups of 8 * n_roles[s] workgroups; workgroup b of the segment
 //       runs role roles[s][(b / 8) % n_roles[s]] of channel-frame 8 (b / (8 n_roles[s])) + b % 8, so
-//       the roles of a frame land on one XCD (blockIdx % 8) and a CU sees the roles mixed
-//   [seg_begin[2], ...)  the resolutions of at most 8192 points (multi; wg_begin relative to seg_begin[2])
-// The K-weighting role counts itself into KWeightParams::kw_done when that is set.
+//       the roles of a frame land on one XCD (blockIdx % 8). (The hardware places an XCD's workgroups
+//       in blockIdx order round-robin over its 4 shader engines and holds the next one until its
+//       engine has room, so with two roles each engine runs one role and the engines of the short
+//       16384-point-resolution workgroups idle ~5 us behind the K-weighting ones: 80 % of the slot-time
+//       used, tools/wgtrace.py. Role chunks of one workgroup per CU fill 90 % of it, but the shader
+//       clock drops from ~2120 to ~1890 MHz and the launch takes longer: the batch runs at the chip's
+//       power limit, so idle slots are not free time. DESIGN.md §8.)
 struct BatchPlan {
   int seg_begin[3];
   int n_roles[2];
   int roles[2][3];
   int mr_res;
   MultiPlan multi;
+  int q_begin, q_n;
 };
 
 // Fused spectrum analysis (cfg3): windowed rfft magnitude (A13) -> log-band max (A10) and raw

@@ -22,9 +22,11 @@
 namespace omega {
 OMEGA_STAMPS_DECL
 OMEGA_WGTRACE_DECL
+OMEGA_MARKS_DECL
 }  // namespace omega
 
 #include "kw.hpp"
+#include "meter_query.hpp"
 #include "regfft.hpp"
 #include "spectral.hpp"
 
@@ -266,6 +268,7 @@ __global__ __launch_bounds__(K / 16, 4) void mrfft_rf_kernel(SpectralParams p, i
 
 OMEGA_STAMPS_GETTER(omega_debug_rf_stamps)
 OMEGA_WGTRACE_GETTER(omega_debug_wgtrace)
+OMEGA_MARKS_GETTER(omega_debug_marks_batch)
 
 hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s) {
   const dim3 grid((unsigned)p.n_cf);
@@ -605,10 +608,44 @@ __device__ __forceinline__ void batch_kw_role(const KWeightParams& kp, int64_t c
   kw_count_in(kp, tid);
 }
 
-__device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, char* smem) {
+// Meter role (workgroup q of the meter segment, the grid's last): wave w computes output
+// o = 8 q + w = (frame o / C, channel o % C). The workgroups are dispatched after every other role of
+// the batch, so their waits cannot hold back the work they wait for: first (bounded) until the meter
+// prep kernel on the side stream has counted in (it has waited for the batch's K-weighting count), then
+// the LUFS meters; then until every true-peak workgroup has counted in, then the true-peak meter
+// (workgroup 0 also rolls the true-peak history). The batch completes only after both, so the caller's
+// stream needs no join kernel and no stream event.
+__device__ __forceinline__ void batch_meter_role(const MeterPrepParams& mp, int q, int tid) {
+  const int64_t o = (int64_t)q * (kBatchThreads / 64) + (tid >> 6);
+  const int64_t f = o / mp.C;
+  const int c = (int)(o % mp.C);
+  const bool valid = f < mp.n_frames;
+  const int lane = tid & 63;
+  OMEGA_MARK(q, 0);
+  if (tid == 0) poll_count(mp.start_ctr, mp.start_target, mp.poll_limit, mp.err_word + 1);
+  __syncthreads();
+  OMEGA_MARK(q, 1);
+  if (valid) meter_query_wave(mp, f, c, lane, true, false);
+  OMEGA_MARK(q, 2);
+  if (tid == 0) poll_count(mp.join_ctr, mp.join_target, mp.poll_limit, mp.err_word + 1);
+  __syncthreads();
+  OMEGA_MARK(q, 3);
+  if (q == 0)
+    for (int ch = 0; ch < mp.C; ++ch) meter_roll_tp(mp, ch, tid, kBatchThreads);
+  if (valid) meter_query_wave(mp, f, c, lane, false, true);
+  OMEGA_MARK(q, 4);
+}
+
+__device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp,
+                                           const MeterPrepParams& mq, char* smem) {
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
   OMEGA_WG_BEGIN();
+  if (b >= bp.q_begin && bp.q_n) {
+    batch_meter_role(mq, b - bp.q_begin, tid);
+    OMEGA_WG_END(4);
+    return;
+  }
   if (b < bp.seg_begin[2]) {
     const int sg = b < bp.seg_begin[1] ? 0 : 1;
     const int j = b - bp.seg_begin[sg], nr = bp.n_roles[sg];
@@ -643,13 +680,15 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
   OMEGA_WG_END(3 + sp.res[r].n);
 }
 
-__global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams sp, KWeightParams kp, BatchPlan bp) {
+__global__ __launch_bounds__(kBatchThreads, 4) void batch_kernel(SpectralParams sp, KWeightParams kp, BatchPlan bp,
+                                                                 MeterPrepParams mq) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  batch_body(sp, kp, bp, smem);
+  batch_body(sp, kp, bp, mq, smem);
 }
 
-hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(batch_kernel, dim3((unsigned)grid), dim3(kBatchThreads), lds_bytes<8192>(), s, sp, kp, bp);
+hipError_t launch_batch(const SpectralParams& sp, const KWeightParams& kp, const BatchPlan& bp, const MeterPrepParams& mq,
+                        int grid, hipStream_t s) {
+  hipLaunchKernelGGL(batch_kernel, dim3((unsigned)grid), dim3(kBatchThreads), lds_bytes<8192>(), s, sp, kp, bp, mq);
   return hipGetLastError();
 }
 

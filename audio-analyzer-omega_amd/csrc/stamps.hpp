@@ -28,14 +28,14 @@
 // << 32, s_memtime at entry, at exit} (the shader clock over the 100 MHz real-time clock gives the
 // clock the workgroup ran at), read by tools/wgtrace.py.
 #define OMEGA_WGTRACE_CAP 65536
-#define OMEGA_WGTRACE_DECL static __device__ unsigned long long g_wgtrace[OMEGA_WGTRACE_CAP * 6];
+#define OMEGA_WGTRACE_DECL static __device__ unsigned long long g_wgtrace[OMEGA_WGTRACE_CAP * 8];
 #define OMEGA_WG_BEGIN()                                                                       \
   const unsigned long long wg_t0_ = __builtin_amdgcn_s_memrealtime();                         \
   const unsigned long long wg_c0_ = __builtin_amdgcn_s_memtime()
 #define OMEGA_WG_END(role)                                                                     \
   do {                                                                                         \
     if (threadIdx.x == 0 && blockIdx.x < OMEGA_WGTRACE_CAP) {                                  \
-      unsigned long long* q_ = g_wgtrace + 6 * (size_t)blockIdx.x;                             \
+      unsigned long long* q_ = g_wgtrace + 8 * (size_t)blockIdx.x;                             \
       q_[5] = __builtin_amdgcn_s_memtime();                                                    \
       q_[1] = __builtin_amdgcn_s_memrealtime();                                                \
       q_[0] = wg_t0_;                                                                          \
@@ -44,6 +44,8 @@
       q_[3] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                  \
               ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);          \
     }                                                                                          \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < OMEGA_WGTRACE_CAP)                             \
+      atomicMax(g_wgtrace + 8 * (size_t)blockIdx.x + 6, __builtin_amdgcn_s_memrealtime());      \
   } while (0)
 #define OMEGA_WGTRACE_GETTER(name)                                                             \
   extern "C" int name(unsigned long long* host) {                                              \
@@ -62,14 +64,14 @@
   } while (0)
 #define OMEGA_STAMPS_GETTER(name)
 #define OMEGA_WGTRACE_CAP 65536
-#define OMEGA_WGTRACE_DECL static __device__ unsigned long long g_wgtrace[OMEGA_WGTRACE_CAP * 6];
+#define OMEGA_WGTRACE_DECL static __device__ unsigned long long g_wgtrace[OMEGA_WGTRACE_CAP * 8];
 #define OMEGA_WG_BEGIN()                                                                       \
   const unsigned long long wg_t0_ = __builtin_amdgcn_s_memrealtime();                         \
   const unsigned long long wg_c0_ = __builtin_amdgcn_s_memtime()
 #define OMEGA_WG_END(role)                                                                     \
   do {                                                                                         \
     if (threadIdx.x == 0 && blockIdx.x < OMEGA_WGTRACE_CAP) {                                  \
-      unsigned long long* q_ = g_wgtrace + 6 * (size_t)blockIdx.x;                             \
+      unsigned long long* q_ = g_wgtrace + 8 * (size_t)blockIdx.x;                             \
       q_[5] = __builtin_amdgcn_s_memtime();                                                    \
       q_[1] = __builtin_amdgcn_s_memrealtime();                                                \
       q_[0] = wg_t0_;                                                                          \
@@ -78,6 +80,8 @@
       q_[3] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                  \
               ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);          \
     }                                                                                          \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < OMEGA_WGTRACE_CAP)                             \
+      atomicMax(g_wgtrace + 8 * (size_t)blockIdx.x + 6, __builtin_amdgcn_s_memrealtime());      \
   } while (0)
 #define OMEGA_WGTRACE_GETTER(name)                                                             \
   extern "C" int name(unsigned long long* host) {                                              \
@@ -103,4 +107,24 @@
   do {                            \
   } while (0)
 #define OMEGA_STAMPS_GETTER(name)
+#endif
+
+// Phase marks of chosen workgroups (trace and stamp builds): s_memrealtime into row `row`, slot k < 8
+// of a per-translation-unit table (tools/wgtrace.py --meters reads the batch's and the meter prep's)
+#if defined(OMEGA_STAMPS) || defined(OMEGA_WGTRACE)
+#define OMEGA_MARKS_DECL static __device__ unsigned long long g_marks[4096 * 8];
+#define OMEGA_MARK(row, k)                                                                     \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && (row) < 4096) g_marks[(row) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define OMEGA_MARKS_GETTER(name)                                                               \
+  extern "C" int name(unsigned long long* host) {                                              \
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_marks), sizeof(g_marks));              \
+  }
+#else
+#define OMEGA_MARKS_DECL
+#define OMEGA_MARK(row, k) \
+  do {                     \
+  } while (0)
+#define OMEGA_MARKS_GETTER(name)
 #endif

@@ -18,7 +18,7 @@ from omega_gpu import _lib as _L  # noqa: E402
 
 _L.use_development_library("libomega_trace.so" if "--trace" in sys.argv else "libomega_dev.so")
 
-ROLE = {0: "kw", 1: "tp", 2: "res16k", 20: "spectra", 3 + 512: "res512", 3 + 1024: "res1k", 3 + 2048: "res2k",
+ROLE = {0: "kw", 1: "tp", 2: "res16k", 4: "meters", 20: "spectra", 3 + 512: "res512", 3 + 1024: "res1k", 3 + 2048: "res2k",
         3 + 4096: "res4k", 3 + 8192: "res8k"}
 
 
@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--probe", type=int, default=None, help="trace omega_dev_probe(which) instead of the batch")
     ap.add_argument("--cfg3", action="store_true", help="trace the cfg3 spectra kernel (4096 frames of 8192)")
     ap.add_argument("--trace", action="store_true", help="the trace-only build (make trace): product registers")
+    ap.add_argument("--meters", action="store_true", help="with the meter aggregates: the prep kernel's and the "
+                    "batch meter role's phase marks on the same clock")
     a = ap.parse_args()
     import bench
     from omega_gpu import NORTHSTAR_RESOLUTIONS, Engine
@@ -39,9 +41,12 @@ def main():
     lib = L.lib()
     eng._bind_stream(x)
     ncf = 2 * F
-    keep = [torch.empty(ncf, 512, device="cuda"), torch.empty(ncf, device="cuda"), torch.empty(ncf, device="cuda")]
+    keep = [torch.empty(ncf, 512, device="cuda"), torch.empty(ncf, device="cuda"), torch.empty(ncf, device="cuda"),
+            torch.empty(ncf, 5, dtype=torch.float64, device="cuda")]
     outs = L.Outputs()
-    outs.combined, outs.lufs_inst, outs.true_peak_db = (t.data_ptr() for t in keep)
+    outs.combined, outs.lufs_inst, outs.true_peak_db = (t.data_ptr() for t in keep[:3])
+    if a.meters:
+        outs.meters = keep[3].data_ptr()
     if a.probe is not None:
         pf = lib.omega_dev_probe
         pf.restype = C.c_int
@@ -63,11 +68,12 @@ def main():
             eng._check(lib.omega_process_frames(eng._ctx, x.data_ptr(), F, 2 * 16384, 16384, C.byref(outs), L.MEM_DEVICE))
     torch.cuda.synchronize()
     cap = 65536
-    buf = (C.c_ulonglong * (cap * 6))()
+    buf = (C.c_ulonglong * (cap * 8))()
     fn = lib.omega_debug_wgtrace
     fn.argtypes = [C.c_void_p]
     assert fn(C.cast(buf, C.c_void_p)) == 0
-    t = np.frombuffer(buf, dtype=np.uint64).reshape(cap, 6)
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(cap, 8)
+    bidx = np.nonzero(t[:, 1] > 0)[0]  # blockIdx of each traced workgroup
     t = t[t[:, 1] > 0]
     t0 = t[:, 0].min()
     beg = (t[:, 0] - t0) / 100.0  # us
@@ -76,6 +82,11 @@ def main():
     hw = (t[:, 3] & 0xFFFFFFFF).astype(np.int64)
     xcc = (t[:, 3] >> 32).astype(np.int64) & 0xF
     cu_key = xcc * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 15)
+    end_all = (t[:, 6].astype(np.float64) - t0) / 100.0  # the last wave's exit
+    for r in sorted(set(role.tolist())):
+        d = (end_all - end)[role == r]
+        print(f"  {ROLE.get(r, r):>7}: last wave exits after wave 0's end mark by p50 {np.median(d):5.2f}  "
+              f"p90 {np.percentile(d, 90):5.2f}  max {d.max():5.2f} us")
     span = end.max()
     clk = (t[:, 5].astype(np.float64) - t[:, 4]) / np.maximum(t[:, 1].astype(np.float64) - t[:, 0], 1) * 100.0
     print(f"workgroups {len(t)}  span {span:.1f} us  CUs {len(np.unique(cu_key))}  shader clock MHz: median "
@@ -106,10 +117,74 @@ def main():
             j = np.searchsorted(b_cu, e)
             if j < len(b_cu):
                 gaps.append(b_cu[j] - e)
+    # the same gaps by (ending role -> next role) on that CU
+    bycat = {}
+    for cu in np.unique(cu_key):
+        sel = np.nonzero(cu_key == cu)[0]
+        sb = sel[np.argsort(beg[sel])]
+        for i in sel:
+            if end[i] > 0.9 * span:
+                continue
+            nxt = sb[beg[sb] >= end[i]]
+            if len(nxt):
+                k = (ROLE.get(role[i], role[i]), ROLE.get(role[nxt[0]], role[nxt[0]]))
+                bycat.setdefault(k, []).append(beg[nxt[0]] - end[i])
+    for k in sorted(bycat, key=lambda k: -len(bycat[k]))[:8]:
+        g = np.array(bycat[k])
+        print(f"    gap {k[0]:>7} -> {k[1]:<7}: n {len(g):4d}  p50 {np.median(g):5.2f}  p90 {np.percentile(g, 90):5.2f} us")
+    for cu in np.unique(cu_key)[:2]:
+        sel = np.nonzero(cu_key == cu)[0]
+        sel = sel[np.argsort(beg[sel])]
+        print(f"    CU {cu}: " + "  ".join(f"{ROLE.get(role[i], role[i])}[{beg[i]:.1f},{end[i]:.1f}]" for i in sel))
     if gaps:
         g = np.array(gaps)
         print(f"  hand-off gaps (us): p10 {np.percentile(g, 10):.2f}  p50 {np.median(g):.2f}  p90 "
               f"{np.percentile(g, 90):.2f}  mean {g.mean():.2f}  over {len(g)} workgroup ends")
+    # dispatch placement: shader engine / CU of XCD 0's first workgroups in blockIdx order
+    se = ((hw >> 13) & 7).astype(int)
+    cu = ((hw >> 8) & 15).astype(int) + 16 * ((hw >> 12) & 1).astype(int)
+    x0 = np.nonzero(xcc == xcc.min())[0]
+    x0 = x0[np.argsort(bidx[x0])][:40]
+    print("  xcd0 placement (blockIdx:role@se.cu):", " ".join(f"{bidx[i]}:{ROLE.get(role[i], role[i])}@{se[i]}.{cu[i]}" for i in x0))
+    print("  shader engines per XCD:", len(np.unique(se[xcc == xcc.min()])), " CUs per SE in xcd0:",
+          [len(np.unique(cu[(xcc == xcc.min()) & (se == e)])) for e in np.unique(se[xcc == xcc.min()])])
+    # per XCD: residency every 4 us (in-order dispatch within an XCD: a slot left empty while the XCD's
+    # next workgroup waits is dispatch latency, not a resource limit)
+    for xc in np.unique(xcc):
+        sx = xcc == xc
+        ncx = len(np.unique(cu_key[sx]))
+        rx = [int(np.sum(sx & (beg <= b) & (end > b))) for b in bins[::4]]
+        print(f"  xcd {xc} ({ncx} CUs, {int(np.sum(sx))} WGs) resident:", " ".join(str(v) for v in rx))
+        bs = beg[sx][np.argsort(bidx[sx])]
+        inv = np.sum(np.diff(bs) < -0.5)
+        print(f"      starts out of blockIdx order by > 0.5 us: {inv} of {len(bs) - 1}")
+    for tb in (6.0, 16.0, 30.0, 60.0):
+        live = (beg <= tb) & (end > tb)
+        per_cu = np.array([np.sum(live & (cu_key == cu)) for cu in np.unique(cu_key)])
+        print(f"  at {tb:4.0f} us: CUs with 0/1/2/3+ resident workgroups: {np.sum(per_cu == 0)}/{np.sum(per_cu == 1)}/"
+              f"{np.sum(per_cu == 2)}/{np.sum(per_cu >= 3)}; next start after it on the idle slots: "
+              f"{np.median([beg[(cu_key == cu) & (beg > tb)].min() - tb for cu in np.unique(cu_key) if np.sum(live & (cu_key == cu)) < 2 and np.any((cu_key == cu) & (beg > tb))] or [0]):.1f} us (median)")
+    if a.meters:
+        def marks(name, rows):
+            f = getattr(lib, name)
+            f.argtypes = [C.c_void_p]
+            mb = (C.c_ulonglong * (4096 * 8))()
+            assert f(C.cast(mb, C.c_void_p)) == 0
+            m = np.frombuffer(mb, dtype=np.uint64).reshape(4096, 8)[:rows].astype(np.float64)
+            return np.where(m > 0, (m - t0) / 100.0, np.nan)
+        pm = marks("omega_debug_marks_meters", 2)
+        for ch in range(2):
+            print(f"  meter prep ch{ch}: start {pm[ch, 0]:6.1f}  K-weighting count met {pm[ch, 1]:6.1f}  "
+                  f"done {pm[ch, 2]:6.1f} us")
+        nq = int(np.sum(role == 4))
+        qm = marks("omega_debug_marks_batch", nq)
+        for k, lab in enumerate(["start", "prep count met", "LUFS meters done", "true-peak count met", "end"]):
+            col = qm[:, k]
+            print(f"  meter role {lab:>20}: min {np.nanmin(col):6.1f}  p50 {np.nanmedian(col):6.1f}  "
+                  f"max {np.nanmax(col):6.1f} us")
+        for r, lab in ((0, "kw"), (1, "tp")):
+            if np.any(role == r):
+                print(f"  last {lab} workgroup ends at {end[role == r].max():6.1f} us")
     first_drop = next((b for b, v in zip(bins, res) if b > 5 and v < 0.9 * full), None)
     print(f"  ramp: {next((b for b, v in zip(bins, res) if v >= 0.95 * full), None)} us to 95 % residency; "
           f"residency below 90 % from {first_drop} us to the end ({span:.1f})")
