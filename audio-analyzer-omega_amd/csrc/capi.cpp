@@ -60,6 +60,11 @@ namespace {
 constexpr double kPi = 3.14159265358979323846;
 constexpr int kChunkFrames = kMeterChunk;
 constexpr int kBatchWaves = 8;  // waves of a batch_kernel workgroup (rfkern.hip kBatchThreads / 64)
+// meter workgroups of the batch grid at most: they wait (spinning) for the meter prep kernel, which
+// needs a whole CU's LDS, so they must never fill every CU (MI355X: 256 CUs, 2 batch slots each; a
+// 4096-frame batch with one meter workgroup per 8 outputs took all 512 slots and waited until the
+// poll bound expired)
+constexpr int kMeterWgs = 64;
 
 struct DevBuf {
   void* p = nullptr;
@@ -242,6 +247,7 @@ struct omega_ctx {
   float* d_wgt[kMaxRes] = {};
   CombEnt* d_ent = nullptr;
   int ent_begin[kMaxRes] = {}, ent_end[kMaxRes] = {};
+  int ent_jmax[kMaxRes] = {};  // the highest bin a resolution's combine entries read (j + 1)
   std::map<std::pair<int, int>, BiquadTab*> kw_tabs;  // (M, chunk) -> device {hp, shelf}
   int rf_sizes = 1 << 14;   // resolution sizes on the register-FFT kernel (bit log2 N): the 16384-point one
   std::map<std::pair<int, int>, float*> windows;  // (m, kind) -> device window
@@ -628,6 +634,8 @@ int build_spectral_tables(omega_ctx* c) {
     c->ent_begin[r] = (int)all.size();
     all.insert(all.end(), er[r].begin(), er[r].end());
     c->ent_end[r] = (int)all.size();
+    c->ent_jmax[r] = 0;
+    for (const CombEnt& en : er[r]) c->ent_jmax[r] = std::max(c->ent_jmax[r], en.j + 1);
   }
   std::vector<int> ooff(1, 0), orj;
   std::vector<float> ofr;
@@ -697,6 +705,7 @@ SpectralParams spectral_params(omega_ctx* c) {
     q.ent_begin = c->ent_begin[r];
     q.ent_end = c->ent_end[r];
     q.cw = (float)c->cfg.res[r].weight;
+    q.low_band = c->ent_jmax[r] < 256;
   }
   p.ent = c->d_ent;
   p.T = c->cfg.target_bins;
@@ -887,7 +896,7 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   // count themselves in, the meter workgroups wait for both; longer batches chain their chunks through
   // the per-context scratch and keep the query kernels
   const bool in_grid = meters && do_tp && do_kw && n_frames > 0 && n_frames <= kChunkFrames;
-  const int64_t n_mq = in_grid ? (n + kBatchWaves - 1) / kBatchWaves : 0;
+  const int64_t n_mq = in_grid ? std::min<int64_t>((n + kBatchWaves - 1) / kBatchWaves, kMeterWgs) : 0;
   bp.q_begin = (int)(end + nwg);
   bp.q_n = (int)n_mq;
   const int64_t grid = end + nwg + n_mq;

@@ -69,17 +69,21 @@ __device__ __forceinline__ void mv4(const float4 m, float a0, float a1, float& r
 }
 
 // One lfilter pass over the block's M samples held as u[L] per thread. REV: the sequence runs from
-// the last sample to the first (the last thread first, each chunk from its end). sin0/1: state
-// entering the first processed sample. On return u holds the outputs and (fin0, fin1) the state
-// after the last processed sample (all threads). pwl[l] = P^(l+1) (LDS). sh: >= 4*NW floats of LDS;
-// the forward and the backward pass use separate halves, so the pass needs a single barrier.
-template <int L, int NTH, bool REV, int SB, bool OPQ = false>
-__device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, const float4* pwl, float sin0,
-                                             float sin1, float* sh, int tid, float& fin0, float& fin1) {
+// the last sample to the first (the last thread first, each chunk from its end). pro(): the state
+// entering the first processed sample (the odd-extension prologue: a serial, wave-uniform chain) --
+// evaluated by wave 0 only and handed to the other waves through LDS with the pass's one barrier. On
+// return u holds the outputs and (fin0, fin1) the state after the last processed sample (all
+// threads). pwl[l] = P^(l+1) (LDS). sh: >= 4*NW + 4 floats of LDS; the forward and the backward pass
+// use separate parts, so the pass needs a single barrier.
+template <int L, int NTH, bool REV, int SB, bool OPQ = false, class Pro>
+__device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, const float4* pwl, Pro pro, float* sh,
+                                             int tid, float& fin0, float& fin1) {
   constexpr int NW = NTH / 64;
   const int lane = tid & 63, wv = tid >> 6;
   const int vl = REV ? 63 - lane : lane;       // position in processing order within the wave
   const int vw = REV ? NW - 1 - wv : wv;       // wave position in processing order
+  float2 si = make_float2(0.f, 0.f);
+  if (wv == 0) si = pro();  // (a uniform branch: the other waves skip the chain)
   // 1) zero-state end state of the chunk (outputs come in step 5): e = sum_i A^(L-1-i) B u_i over the
   // chunk's samples in processing order -- two independent dot products whose coefficients are LDS
   // broadcast reads (pwl[64 + j].zw), instead of the serial state recurrence (4 dependent VALU ops per
@@ -135,12 +139,18 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
   // 3) wave totals -> the carry into this wave and the pass's final state, from all wave totals
   OMEGA_STAMP(SB + 1);
   float* shp = sh + (REV ? 2 * NW : 0);
+  float* sio = sh + 4 * NW + (REV ? 2 : 0);
   if (vl == 63) {
     shp[2 * vw] = s0;
     shp[2 * vw + 1] = s1;
   }
+  if (wv == 0 && lane == 0) {
+    sio[0] = si.x;
+    sio[1] = si.y;
+  }
   __syncthreads();
   OMEGA_STAMP(SB + 2);
+  const float sin0 = sio[0], sin1 = sio[1];
   float c0 = sin0, c1 = sin1, k0 = sin0, k1 = sin1;
   static_for<0, NW>([&](auto w) {
     if (w == vw) {
@@ -191,22 +201,34 @@ __device__ __forceinline__ void filtfilt(float (&u)[L], const BiquadTab* __restr
                                          float* sh, int tid) {
   static_assert(E >= 1 && E <= 9, "the gathered edges cover 10 samples per side");
   const BqRegs t = bq_regs(tg);
-  // left odd extension ext[i] = 2u[0] - u[E-i], i < E (formed in float32, as scipy does for f32)
-  const float u0 = e[0], uN = e[19];
-  float s0 = t.zi0 * (2.f * u0 - e[E]), s1 = t.zi1 * (2.f * u0 - e[E]);
-#pragma unroll
-  for (int i = 0; i < E; ++i) bq_step(t, 2.f * u0 - e[E - i], s0, s1);
   float f0, f1;
-  lfilter_pass<L, NTH, false, SB, OPQ>(u, t, pwl, s0, s1, sh, tid, f0, f1);
+  // left odd extension ext[i] = 2u[0] - u[E-i], i < E (formed in float32, as scipy does for f32)
+  lfilter_pass<L, NTH, false, SB, OPQ>(
+      u, t, pwl,
+      [&]() {
+        const float u0 = e[0];
+        float s0 = t.zi0 * (2.f * u0 - e[E]), s1 = t.zi1 * (2.f * u0 - e[E]);
+#pragma unroll
+        for (int i = 0; i < E; ++i) bq_step(t, 2.f * u0 - e[E - i], s0, s1);
+        return make_float2(s0, s1);
+      },
+      sh, tid, f0, f1);
   // right odd extension ext[M+E+i] = 2u[M-1] - u[M-2-i]: forward outputs, then the backward start
-  float yr[E];
+  const float g0 = f0, g1 = f1;
+  lfilter_pass<L, NTH, true, SB + 5, OPQ>(
+      u, t, pwl,
+      [&]() {
+        const float uN = e[19];
+        float r0 = g0, r1 = g1;
+        float yr[E];
 #pragma unroll
-  for (int i = 0; i < E; ++i) yr[i] = bq_step(t, 2.f * uN - e[18 - i], f0, f1);
-  s0 = t.zi0 * yr[E - 1];
-  s1 = t.zi1 * yr[E - 1];
+        for (int i = 0; i < E; ++i) yr[i] = bq_step(t, 2.f * uN - e[18 - i], r0, r1);
+        float s0 = t.zi0 * yr[E - 1], s1 = t.zi1 * yr[E - 1];
 #pragma unroll
-  for (int i = E - 1; i >= 0; --i) bq_step(t, yr[i], s0, s1);
-  lfilter_pass<L, NTH, true, SB + 5, OPQ>(u, t, pwl, s0, s1, sh, tid, f0, f1);
+        for (int i = E - 1; i >= 0; --i) bq_step(t, yr[i], s0, s1);
+        return make_float2(s0, s1);
+      },
+      sh, tid, f0, f1);
 }
 
 template <int L, int NTH, bool OPQ = false>
@@ -248,7 +270,7 @@ __device__ __forceinline__ void kw_count_in(const KWeightParams& p, int tid) {
 
 // K-weighting of channel-frame cf by a workgroup of NTH threads (all of them), chunk L = M / NTH
 // (the host tables must be built for that L). LDS from the caller: pwl[2][kPwl] scan tables, fbuf[M]
-// parking for f (element-major), sh[4 * NW], edge[20], red[NW].
+// parking for f (element-major), sh[4 * NW + 4], edge[20], red[NW].
 template <int M, int NTH, bool PUB = false, bool OPQ = false>
 __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf, int tid, float4 (*pwl)[kPwl], float* fbuf,
                                              float* sh, float* edge, double* red) {

@@ -41,7 +41,7 @@ __global__ __launch_bounds__(NTH, kw_waves_per_eu(NTH)) void kweight_kernel(KWei
   static_assert(M / NTH == kw_chunk(M), "chunk length must match the host tables");
   __shared__ float4 pwl[2][kPwl];  // scan powers and A^i rows of both filters (kw.hpp)
   __shared__ float fbuf[M];      // f, element-major (fbuf[i * NTH + t]): conflict-free, own data only
-  __shared__ float sh[4 * NW];
+  __shared__ float sh[4 * NW + 4];
   __shared__ float edge[20];
   __shared__ double red[NW];
   kweight_body<M, NTH, PUB>(p, blockIdx.x, threadIdx.x, pwl, fbuf, sh, edge, red);

@@ -24,6 +24,8 @@ struct ResParam {
   float* mag_out;        // [n_cf, N_r/2+1] or nullptr
   int ent_begin, ent_end;  // this resolution's combine entries
   float cw;              // combine weight (config.weight)
+  int low_band;          // the entries read only bins < 256 (the 16384-point register FFT then forms
+                         // just the lowest and highest 256 frequencies: RegFFT::run_low)
 };
 
 struct SpectralParams {

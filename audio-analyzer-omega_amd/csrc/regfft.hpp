@@ -171,6 +171,60 @@ struct RegFFT {
     }
   }
 
+  // run() for a consumer that reads only the lowest 256 and the highest 256 frequencies (K = 8192:
+  // pass-3 outputs c = m + 16 q = 0 and 31 of every (k1, k2)), stored straight to their
+  // natural-order slots a3(n): pass 3 forms just those two sums of its 32 inputs (F_q[0] and
+  // F_q[15] of the lane pair's halves, joined by one DPP exchange) instead of the DFT16 and the
+  // radix-2 step, and each lane writes one value instead of 16. On return the two bands are in `buf`
+  // (published by a barrier); the other slots hold exchange-2 data.
+  template <bool SYNC = false, bool LT2 = false>
+  static __device__ __forceinline__ void run_low(float2 (&v)[16], float2* buf, int t, float2 w1, float2 w2,
+                                                 const float2* t2 = nullptr) {
+    static_assert(L == 32, "the two-band pass 3 is the K = 8192 plan");
+    // passes 1 and 2 as in run2
+    dft16(v);
+    twiddle(v, w1);
+    if constexpr (SYNC) __syncthreads();
+    {
+      float2* b = buf + t;
+      static_for<0, 16>([&](auto k1) { b[P1 * k1] = v[k1]; });
+    }
+    __syncthreads();
+    {
+      const int u = t % L, k1 = t / L;
+      const float2* b = buf + P1 * k1 + u;
+      static_for<0, 16>([&](auto r) { v[r] = b[L * r]; });
+      dft16(v);
+      if constexpr (LT2)
+        twiddle_t2(v, t2 + u);
+      else
+        twiddle(v, w2);
+      __syncthreads();
+      float2* bw = buf + P2R * k1 + u;
+      static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
+    }
+    __syncthreads();
+    const int q = t & 1, k2 = (t >> 1) & 15, k1 = t >> 5;
+    {
+      const float2* b = buf + P2R * k1 + P2C * k2 + q;
+      static_for<0, 16>([&](auto r) { v[r] = b[2 * r]; });
+    }
+    // F_q[0] = sum_u' c[u'], F_q[15] = sum_u' c[u'] W16^{15 u'}
+    float2 f0 = v[0], f15 = v[0];
+    static_for<1, 16>([&](auto r) {
+      f0 = cadd(f0, v[r]);
+      f15 = cadd(f15, twc<15 * r, 16>(v[r]));
+    });
+    // X_0 = F_0[0] + F_1[0] (even lane), X_31 = F_0[15] - W32^15 F_1[15] (odd lane)
+    const float2 g = twc<15, 32>(f15);
+    const float2 send = q ? f0 : f15;
+    const float2 recv = make_float2(lane_xor1(send.x), lane_xor1(send.y));
+    const float2 out = q ? csub(recv, g) : cadd(f0, recv);
+    __syncthreads();  // every exchange-2 read is done
+    buf[s3o(t) + (q ? o3o(15) : 0)] = out;
+    __syncthreads();
+  }
+
   // Natural-order spectrum exchange after run(): every register to its frequency's slot
   // (the caller synchronises before, if the buffer may still be read, and after).
   static __device__ __forceinline__ void store_spectrum(const float2 (&v)[16], float2* buf, int t) {

@@ -205,10 +205,48 @@ __device__ __forceinline__ void mrfft_rf_body(const SpectralParams& p, int r, in
   const int e0 = rp.ent_begin + t;
   CombEnt ent{};
   if (p.comb_out && e0 < rp.ent_end) ent = p.ent[e0];
-  FFT::template run<false, true>(v, buf, t, w1, w2b, t2);
-  __syncthreads();
-  FFT::store_spectrum(v, buf, t);
-  __syncthreads();
+  bool low = false;
+  if constexpr (K == 8192) low = !rp.mag_out && rp.low_band;
+  if (low) {
+    if constexpr (K == 8192) FFT::template run_low<false, true>(v, buf, t, w1, w2b, t2);
+  } else {
+    FFT::template run<false, true>(v, buf, t, w1, w2b, t2);
+    __syncthreads();
+    FFT::store_spectrum(v, buf, t);
+    __syncthreads();
+  }
+  if (!rp.mag_out) {
+    // combine only (no magnitude output): each entry untangles the two bins it reads straight from the
+    // natural-order packed spectrum -- the combine reads a few hundred of the K + 1 bins, so the
+    // per-thread untangle + |.| of all of them and the magnitude round trip through LDS are skipped
+    if (!p.comb_out) return;
+    auto mag_at = [&](int j) -> float {  // |X_j|, 0 <= j <= K
+      const float2 a = buf[FFT::a3(j == K ? 0 : j)];
+      if (j == 0) return fabsf(a.x + a.y);
+      if (j == K) return fabsf(a.x - a.y);
+      if (j == K / 2) return cabs(a);  // X[K/2] = conj(Z[K/2])
+      const float2 b = buf[FFT::a3(K - j)];
+      float2 xk, xkk;
+      untangle(a, b, twM[j], xk, xkk);
+      return cabs(xk);
+    };
+    float* o = p.comb_out + cf * p.T;
+    auto apply = [&](const CombEnt& en) {
+      const int tt = en.tm & 0xFFFFFF, op = en.tm >> 24;
+      if (op == 2) {
+        o[tt] = 0.f;
+        return;
+      }
+      const float val = fmaf(en.c1, mag_at(en.j + 1), en.c0 * mag_at(en.j));
+      if (op == 0)
+        o[tt] = val;
+      else
+        o[tt] += val;
+    };
+    if (e0 < rp.ent_end) apply(ent);
+    for (int e = e0 + NTH; e < rp.ent_end; e += NTH) apply(p.ent[e]);
+    return;
+  }
   float mg[16];
   float mnyq = 0.f;
   {
@@ -592,47 +630,47 @@ __device__ __forceinline__ void batch_multi(const SpectralParams& p, int r, int6
   mrfft_frame<K, G>(p, r, valid ? cf : p.n_cf - 1, valid, tid % G, smem + grp * K);
 }
 
-// K-weighting role (kweight_kernel's LDS, carved: pwl 3 KiB | fbuf 64 KiB | sh 32 floats | edge 20
+// K-weighting role (kweight_kernel's LDS, carved: pwl 3 KiB | fbuf 64 KiB | sh 36 floats | edge 20
 // floats | red 8 doubles)
 __device__ __forceinline__ void batch_kw_role(const KWeightParams& kp, int64_t cf, int tid, char* smem) {
   constexpr int kP = 2 * kPwl * 16;  // pwl bytes
   auto* pwl = reinterpret_cast<float4(*)[kPwl]>(smem);
   float* fbuf = reinterpret_cast<float*>(smem + kP);
   float* sh = reinterpret_cast<float*>(smem + kP + 65536);
-  float* edge = sh + 32;
-  double* red = reinterpret_cast<double*>(smem + kP + 65536 + 208);
-  static_assert(kP + 65536 + 208 + 64 <= lds_bytes<8192>(), "K-weighting role LDS");
+  float* edge = sh + 36;
+  double* red = reinterpret_cast<double*>(smem + kP + 65536 + 224);
+  static_assert(kP + 65536 + 224 + 64 <= lds_bytes<8192>(), "K-weighting role LDS");
   // (one instantiation: the value is always stored write-through; a second copy of the body costs
   // the kernel another set of spill slots)
   kweight_body<16384, kBatchThreads, true, true>(kp, cf, tid, pwl, fbuf, sh, edge, red);
   kw_count_in(kp, tid);
 }
 
-// Meter role (workgroup q of the meter segment, the grid's last): wave w computes output
-// o = 8 q + w = (frame o / C, channel o % C). The workgroups are dispatched after every other role of
-// the batch, so their waits cannot hold back the work they wait for: first (bounded) until the meter
-// prep kernel on the side stream has counted in (it has waited for the batch's K-weighting count), then
-// the LUFS meters; then until every true-peak workgroup has counted in, then the true-peak meter
-// (workgroup 0 also rolls the true-peak history). The batch completes only after both, so the caller's
-// stream needs no join kernel and no stream event.
-__device__ __forceinline__ void batch_meter_role(const MeterPrepParams& mp, int q, int tid) {
-  const int64_t o = (int64_t)q * (kBatchThreads / 64) + (tid >> 6);
-  const int64_t f = o / mp.C;
-  const int c = (int)(o % mp.C);
-  const bool valid = f < mp.n_frames;
+// Meter role (workgroup q of the nq of the meter segment, the grid's last): wave w computes outputs
+// o = 8 q + w, 8 q + w + 8 nq, ... = (frame o / C, channel o % C). The workgroups are dispatched after
+// every other role of the batch, so their waits cannot hold back the batch work they wait for: first
+// (bounded) until the meter prep kernel on the side stream has counted in (it has waited for the
+// batch's K-weighting count), then the LUFS meters; then until every true-peak workgroup has counted
+// in, then the true-peak meter (workgroup 0 also rolls the true-peak history). The batch completes only
+// after both, so the caller's stream needs no join kernel and no stream event. nq is at most
+// kMeterWgs (the host's cap): the waiting workgroups must leave CUs free for the prep kernel, which
+// needs a whole CU's LDS and may be dispatched after them.
+__device__ __forceinline__ void batch_meter_role(const MeterPrepParams& mp, int q, int nq, int tid) {
+  const int64_t n_out = mp.n_frames * mp.C, step = (int64_t)nq * (kBatchThreads / 64);
+  const int64_t o0 = (int64_t)q * (kBatchThreads / 64) + (tid >> 6);
   const int lane = tid & 63;
   OMEGA_MARK(q, 0);
   if (tid == 0) poll_count(mp.start_ctr, mp.start_target, mp.poll_limit, mp.err_word + 1);
   __syncthreads();
   OMEGA_MARK(q, 1);
-  if (valid) meter_query_wave(mp, f, c, lane, true, false);
+  for (int64_t o = o0; o < n_out; o += step) meter_query_wave(mp, o / mp.C, (int)(o % mp.C), lane, true, false);
   OMEGA_MARK(q, 2);
   if (tid == 0) poll_count(mp.join_ctr, mp.join_target, mp.poll_limit, mp.err_word + 1);
   __syncthreads();
   OMEGA_MARK(q, 3);
   if (q == 0)
     for (int ch = 0; ch < mp.C; ++ch) meter_roll_tp(mp, ch, tid, kBatchThreads);
-  if (valid) meter_query_wave(mp, f, c, lane, false, true);
+  for (int64_t o = o0; o < n_out; o += step) meter_query_wave(mp, o / mp.C, (int)(o % mp.C), lane, false, true);
   OMEGA_MARK(q, 4);
 }
 
@@ -642,7 +680,7 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
   const int b = blockIdx.x;
   OMEGA_WG_BEGIN();
   if (b >= bp.q_begin && bp.q_n) {
-    batch_meter_role(mq, b - bp.q_begin, tid);
+    batch_meter_role(mq, b - bp.q_begin, bp.q_n, tid);
     OMEGA_WG_END(4);
     return;
   }

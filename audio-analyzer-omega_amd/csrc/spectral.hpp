@@ -81,6 +81,40 @@ __device__ __forceinline__ void mrfft_frame(const SpectralParams& p, int r, int6
     return make_float2(a.x * w.x, a.y * w.y);
   });
   OMEGA_STAMP(11 + 4 * (ilog2(K) - 9));
+  if (!rp.mag_out) {
+    // combine only (no magnitude output; uniform over the workgroup's groups): each entry untangles
+    // the two bins it reads straight from the packed spectrum -- the combine reads a few hundred of
+    // the K + 1 bins, so the all-bin magnitude pass and its barrier are skipped
+    if (!valid || !p.comb_out) return;
+    const float2* __restrict__ twN = p.tw[ilog2(2 * K)];
+    auto mag_at = [&](int j) -> float {  // |X_j|, 0 <= j <= K
+      const float2 a = buf[FFT::out(j == K ? 0 : j)];
+      if (j == 0) return fabsf(a.x + a.y);
+      if (j == K) return fabsf(a.x - a.y);
+      if (j == K / 2) return cabs(a);  // X[K/2] = conj(Z[K/2])
+      float2 xk, xkk;
+      untangle(a, buf[FFT::out(K - j)], twN[j], xk, xkk);
+      return cabs(xk);
+    };
+    float* o = p.comb_out + cf * p.T;
+    auto apply = [&](const CombEnt& en) {
+      const int t = en.tm & 0xFFFFFF, op = en.tm >> 24;
+      if (op == 2) {
+        o[t] = 0.f;
+        return;
+      }
+      const float v = fmaf(en.c1, mag_at(en.j + 1), en.c0 * mag_at(en.j));
+      if (op == 0)
+        o[t] = v;
+      else
+        o[t] += v;
+    };
+    static_for<0, EP>([&](auto i) {
+      if (rp.ent_begin + tid + i * NTH < rp.ent_end) apply(ent[i]);
+    });
+    for (int e = rp.ent_begin + tid + EP * NTH; e < rp.ent_end; e += NTH) apply(p.ent[e]);
+    return;
+  }
   rfft_magnitudes<K, NTH>(buf, p.tw[ilog2(2 * K)], tid);
   OMEGA_STAMP(12 + 4 * (ilog2(K) - 9));
   if (!valid) return;

@@ -480,6 +480,21 @@ def test_cfg2_sampled_frames_match_oracle(cfg2):
         assert abs(out["true_peak_db"][cf] - tp) < TP_TOL_DB
 
 
+def test_cfg2_combine_only_matches_magnitude_path(cfg2):
+    """Without magnitude outputs the batch's resolutions combine straight from the packed spectra (the
+    16384-point one forms only its lowest and highest 256 frequencies, RegFFT::run_low); with them, every
+    bin's magnitude is formed first. Both must give the same combined spectrum on all 512 channel-frames
+    (float32 rounding apart: the two paths take the untangle twiddles from different forms)."""
+    import torch
+    x, eng, xd, out = cfg2
+    eng.reset_meters()
+    full = eng.process_frames(xd, 256, 2 * 16384, 16384, mags=True)
+    torch.cuda.synchronize()
+    fc = full["combined"].cpu().numpy()
+    err = np.abs(fc - out["combined"]).max(axis=1) / np.abs(fc).max(axis=1)
+    assert err.max() < 1e-5, err.max()
+
+
 def test_cfg2_properties(cfg2):
     import torch
     x, eng, xd, out = cfg2
