@@ -50,24 +50,38 @@ def main(rnd):
     # roofline probe's 3 + 20 back-to-back launches without the meter kernels beside it; the cfg5 stream
     # uses other grids
     bk = [r for r in rows if short(r["Kernel_Name"]) == TP]
+    bk.sort(key=lambda r: int(r["Start_Timestamp"]))
     steps = 25
     if bk:
+        dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in bk]
         grids = [r["Grid_Size_X"] for r in bk]
-        g0 = max(set(grids), key=grids.count)
-        cfg2 = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in bk if r["Grid_Size_X"] == g0]
-        pipe, timed = cfg2[:steps], cfg2[steps + 3:steps + 23]
-        lines += ["", f"Batch kernel `{TP}` (all per-channel-frame work of a step in one launch), cfg2 grid {g0}:", "",
-                  f"- in the pipeline (the meter kernels run beside it on a side stream): {len(pipe)} dispatches, "
-                  f"avg {sum(pipe) / len(pipe):.1f} us",
-                  f"- roofline probe (alone, back to back; bench.py `roofline.kernel_ms` times these 20 with HIP "
-                  f"events): {len(timed)} dispatches, avg {sum(timed) / max(1, len(timed)):.1f} us"]
-        others = {}
-        for r in bk:
-            if r["Grid_Size_X"] != g0:
-                others.setdefault(r["Grid_Size_X"], []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-        for gsz, v in others.items():
-            lines.append(f"- grid {gsz} (another bench leg: cfg4 launches 8192 channel-frames, the cfg5 stream and the ingest tests smaller batches): {len(v)} "
-                         f"dispatches, avg {sum(v) / len(v):.1f} us")
+        # the roofline probe: the first run of 23 back-to-back dispatches of one grid (3 warm-up + 20)
+        # that follows 25 pipeline steps (5 warmup + 20 timed; since round 3 their grid carries the meter
+        # segment, so it differs from the probe's)
+        runs, i = [], 0  # (grid, first index, length) of the runs of equal grids
+        while i < len(grids):
+            j = i
+            while j < len(grids) and grids[j] == grids[i]:
+                j += 1
+            runs.append((grids[i], i, j - i))
+            i = j
+        i0 = next((runs[k][1] for k in range(1, len(runs)) if runs[k][2] == 23 and runs[k - 1][2] >= steps), None)
+        if i0 is not None:
+            pipe, timed = dur[i0 - steps:i0], dur[i0 + 3:i0 + 23]
+            gp, gt = grids[i0 - 1], grids[i0]
+            lines += ["", f"Batch kernel `{TP}` (all per-channel-frame work of a step in one launch), cfg2:", "",
+                      f"- in the pipeline (grid {gp}: the step's launch with the meter segment; the meter prep "
+                      f"kernel on the side stream): {len(pipe)} dispatches, avg {sum(pipe) / len(pipe):.1f} us",
+                      f"- roofline probe (grid {gt}: no meters, back to back; bench.py `roofline.kernel_ms` times "
+                      f"these 20 with HIP events): {len(timed)} dispatches, avg {sum(timed) / max(1, len(timed)):.1f} us"]
+            used = set(range(i0 - steps, i0 + 23))
+            others = {}
+            for i, r in enumerate(bk):
+                if i not in used:
+                    others.setdefault(r["Grid_Size_X"], []).append(dur[i])
+            for gsz, v in others.items():
+                lines.append(f"- grid {gsz} (other bench legs: cfg4 launches of 8192 channel-frames, the cfg1 / "
+                             f"latency lines, the cfg5 stream): {len(v)} dispatches, avg {sum(v) / len(v):.1f} us")
     b = json.loads([ln for ln in open(os.path.join(SRC, "stats.json")) if ln.startswith("{")][-1]) \
         if os.path.exists(os.path.join(SRC, "stats.json")) else json.load(open(os.path.join(SRC, "bench.json")))
     lines += ["", f"bench.py in the profiled run: roofline.kernel_ms = {b['roofline']['kernel_ms'] * 1e3:.1f} us, "
