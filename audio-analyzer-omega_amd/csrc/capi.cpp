@@ -897,6 +897,8 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   // the per-context scratch and keep the query kernels
   const bool in_grid = meters && do_tp && do_kw && n_frames > 0 && n_frames <= kChunkFrames;
   const int64_t n_mq = in_grid ? std::min<int64_t>((n + kBatchWaves - 1) / kBatchWaves, kMeterWgs) : 0;
+  // the grid's last segment (measured: placed before the small resolutions it holds 64 slots from
+  // ~50 us on and the step is no shorter, 77.4-79.2 vs 77.0-78.0 us)
   bp.q_begin = (int)(end + nwg);
   bp.q_n = (int)n_mq;
   const int64_t grid = end + nwg + n_mq;

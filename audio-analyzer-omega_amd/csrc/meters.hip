@@ -137,6 +137,27 @@ __device__ __forceinline__ Scan4 block_excl_scan4(const Scan4& x, int* wsa, int*
   return Scan4{rl(sa) + ia - x.a, rl(sb) + ib - x.b, rl(sc) + ic - x.c, rld(sd) + id - x.d};
 }
 
+// Write-through (agent-scope relaxed atomic) stores of the prep outputs the in-grid meter queries read
+// on other XCDs: with every such store drained, a relaxed counter add publishes them -- no release
+// fence, whose L2 write-back took 4-11 us after the prep's last store in the batch's workgroup trace.
+__device__ __forceinline__ void st_wt(float* q, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(q), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(int* q, int v) {
+  __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(double* q, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(q), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(MeterExt* q, const MeterExt& e) {
+  unsigned long long* d = reinterpret_cast<unsigned long long*>(q);
+  __hip_atomic_store(d, (unsigned long long)__float_as_uint(e.v) | ((unsigned long long)e.t << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(d + 1, (unsigned long long)(unsigned)e.rc | ((unsigned long long)(unsigned)e.pad << 32),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The stream's LUFS_inst sequence over [T0 - nh, T0 + F) lives in LDS (V); every global input is
 // fetched once, up front.
 __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
@@ -360,9 +381,9 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     if (u < G) {
       const unsigned long long k = U[u];
       if (in_core(k)) {
-        core[ec++] = unkey((uint32_t)(k >> 32));
+        st_wt(core + ec++, unkey((uint32_t)(k >> 32)));
       } else {
-        ext[ee++] = MeterExt{unkey((uint32_t)(k >> 32)), (uint32_t)k, ec, 0};
+        st_wt(ext + ee++, MeterExt{unkey((uint32_t)(k >> 32)), (uint32_t)k, ec, 0});
       }
     }
   }
@@ -371,8 +392,8 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   for (int q = 0; q < pv; ++q) {
     const int u = v0 + q;
     if (u < L) {
-      gp[u] = eg;
-      gsum[u] = ed;
+      st_wt(gp + u, eg);
+      st_wt(gsum + u, ed);
       if (V[u] > gate) {
         ++eg;
         ed += (double)V[u];
@@ -380,21 +401,21 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     }
   }
   if (v0 < L && v0 + pv >= L) {  // the run that ends the sequence holds the totals
-    gp[L] = eg;
-    gsum[L] = ed;
+    st_wt(gp + L, eg);
+    st_wt(gsum + L, ed);
   }
   if (u0 < G && u0 + pu >= G) {
-    p.n_core[c] = ec;
-    p.n_ext[c] = ee;
+    st_wt(p.n_core + c, ec);
+    st_wt(p.n_ext + c, ee);
   }
   if (tid == 0) {
     if (L == 0) {
-      gp[0] = 0;
-      gsum[0] = 0.0;
+      st_wt(gp, 0);
+      st_wt(gsum, 0.0);
     }
     if (G == 0) {
-      p.n_core[c] = 0;
-      p.n_ext[c] = 0;
+      st_wt(p.n_core + c, 0);
+      st_wt(p.n_ext + c, 0);
     }
     p.n_s_out[c] = Ka + Kb;
     p.t0_out[c] = T0 + (uint32_t)F;
@@ -407,15 +428,11 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   OMEGA_STAMP(7);
   OMEGA_MARK(c, 2);
   if (p.q_done) {
-    // (tail layout) count this channel's prep in for the query kernel on the other stream: every
-    // wave's stores drained, then one agent-scope release before the add
+    // count this channel's prep in for the batch's meter segment: every wave's (write-through) stores
+    // drained, then a relaxed add
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_fetch_add(p.q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (tid == 0) __hip_atomic_fetch_add(p.q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

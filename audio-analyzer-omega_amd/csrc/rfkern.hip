@@ -679,7 +679,7 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
   OMEGA_WG_BEGIN();
-  if (b >= bp.q_begin && bp.q_n) {
+  if (b >= bp.q_begin && b < bp.q_begin + bp.q_n) {
     batch_meter_role(mq, b - bp.q_begin, bp.q_n, tid);
     OMEGA_WG_END(4);
     return;
