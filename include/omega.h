@@ -128,9 +128,10 @@ int omega_set_stream(omega_ctx* ctx, void* hip_stream);
 /* flags: bit 0 = HIP graphs: device-memory omega_process_frames calls are captured once per distinct
  * argument set and replayed afterwards (default off: measured slower than direct launches on MI355X,
  * see DESIGN.md); bits 1-2 = stream layout:
- * 0 default: 16384-sample frames on direct launches run as ONE batch kernel (K-weighting, true peak
- * and every resolution as workgroup roles of one grid) with the meter aggregates on a side stream that
- * is ordered by device counters instead of stream events; other calls (and graph capture) as below;
+ * 0 default: 16384-sample frames on direct launches run as ONE batch kernel (K-weighting, true peak,
+ * every resolution and -- up to 2048 frames per channel -- the meter aggregates as workgroup roles of
+ * one grid) with the meter prep on a side stream ordered by device counters instead of stream events;
+ * other calls (and graph capture) as below;
  * any other value: the full-chip kernels back to back on the stream, the latency-bound meter prep and
  * LUFS query kernels on a side stream joined by events. Every layout gives the same outputs bitwise. */
 int omega_set_graphs(omega_ctx* ctx, int flags);
