@@ -416,12 +416,13 @@ def drums_line(dev, reps=20, n=4096, bins=1025):
     ms = s.elapsed_time(e) / reps
     bpf = 4 * bins + 8 * 14
     gbs = n * bpf / (ms * 1e-3) / 1e9
+    traffic, src = kernel_traffic("drums")
     return {"workload": f"drum features: {n} consecutive frames x {bins} bins of one stream (kick 3 + snare 4 band "
                         "flux, adaptive thresholds, spectral centroid)",
             "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_call": ms,
             "roofline": {"bound": "latency", "kernel": "drum_flux_kernel + drum_thr_kernel", "achieved": gbs,
-                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
-                         "bytes_per_frame": bpf}}
+                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": traffic,
+                         "traffic_source": src, "bytes_per_frame": bpf}}
 
 
 def post_line(dev, reps=20, n=4096, bins=512):
@@ -444,12 +445,13 @@ def post_line(dev, reps=20, n=4096, bins=512):
     ms = s.elapsed_time(e) / reps
     bpf = 4 * (2 * bins + 1) + 8 * pp.n_bands
     gbs = n * bpf / (ms * 1e-3) / 1e9
+    traffic, src = kernel_traffic("post")
     return {"workload": f"app post-processing: {n} consecutive combined spectra x {bins} bins of one stream "
                         f"({pp.n_bands} bands)",
             "value": n / (ms * 1e-3), "unit": "frames/s", "ms_per_call": ms,
             "roofline": {"bound": "latency", "kernel": "post_frame_kernel + post_ema_kernel", "achieved": gbs,
-                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": None,
-                         "bytes_per_frame": bpf}}
+                         "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": gbs / PEAK_HBM_GBS, "traffic": traffic,
+                         "traffic_source": src, "bytes_per_frame": bpf}}
 
 
 def cfg5_line(rank, world, dev, seconds=60.0):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one stage of the cfg2 hot path in isolation (for rocprofv3 counter passes and A/B timing).
 
-  python tools/kernel_bench.py {batch,tp,kw,mrfft,meters,all,host,spectra} [--reps N]
+  python tools/kernel_bench.py {batch,tp,kw,mrfft,meters,all,host,spectra,drums,post} [--reps N]
 """
 import argparse
 import os
@@ -51,6 +51,17 @@ def main():
         so = {"bands": torch.empty(4096, 512, device="cuda"),
               "chroma": torch.empty(4096, 12, dtype=torch.float64, device="cuda")}
 
+    if a.stage == "drums":  # bench.py drums_line's call: 4096 magnitude frames x 1025 bins of one stream
+        rng = np.random.default_rng(5)
+        dmag = torch.from_numpy(np.abs(rng.standard_normal((4096, 1025))).astype(np.float32)).cuda()
+        deng = Engine(sample_rate=48000)
+        dout = torch.empty(4096, 14, dtype=torch.float64, device="cuda")
+    if a.stage == "post":  # bench.py post_line's call: 4096 combined spectra x 512 bins of one stream
+        from omega_gpu.app_post import SpectrumPostProcessor
+        rng = np.random.default_rng(6)
+        px = torch.from_numpy(rng.random((4096, 512)).astype(np.float32)).cuda()
+        pp = SpectrumPostProcessor(np.linspace(20, 20000, 512))
+
     outs = L.Outputs()
     outs.combined, outs.lufs_inst, outs.true_peak_db = comb.data_ptr(), out["li"].data_ptr(), out["tp"].data_ptr()
 
@@ -61,6 +72,10 @@ def main():
                                                 L.MEM_DEVICE))
         if a.stage == "spectra":
             e3.spectra(x3, "hann", bands=bt, chroma=True, out=so)
+        if a.stage == "drums":
+            deng.drum_features(dmag, out=dout)
+        if a.stage == "post":
+            pp.process(px)
         if a.stage == "host":  # host buffers in and out: PCIe-inclusive rate of the full path
             host_out.update(eng.process_frames(xh, 256, 2 * 16384, 16384, meters=True))
         if a.stage in ("tp", "all"):

@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json
 cat $OUT/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o bench --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/stats.json 2> $OUT/stats.log
-for stage in batch spectra; do
+for stage in batch spectra drums post; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_${stage}_$c -o run -- python tools/kernel_bench.py $stage --reps 20 > $OUT/pmc_${stage}_$c.log 2>&1
   done

@@ -87,19 +87,38 @@ def main(rnd):
     lines += ["", f"bench.py in the profiled run: roofline.kernel_ms = {b['roofline']['kernel_ms'] * 1e3:.1f} us, "
                   f"value = {b['value']:.0f} {b['unit']}, ms_per_step = {b['ms_per_step']:.4f}"]
     open(os.path.join(dst, f"r{rnd}_bench_dispatches.md"), "w").write("\n".join(lines) + "\n")
+    # (stage, kernels of one call, tag, algorithmic bytes per call, command); a call of several kernels
+    # sums their per-dispatch averages (drums: flux + thresholds; post: frame + EMA + check + fix)
     for stage, kname, tag, alg, cmd in (
             ("batch", TP, "batch", 512 * (16384 * 4 + 4 * (512 + 2)), "batch --reps 20"),
-            ("spectra", "spectra_rf_kernel", "cfg3", 4096 * (8192 * 4 + 4 * (512 + 12)), "spectra --reps 20")):
+            ("spectra", "spectra_rf_kernel", "cfg3", 4096 * (8192 * 4 + 4 * (512 + 12)), "spectra --reps 20"),
+            ("drums", "drum_", "drums", 4096 * (4 * 1025 + 8 * 14), "drums --reps 20"),
+            ("post", "post_", "post", None, "post --reps 20")):
         tr = {}
+        ok = True
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(SRC, f"pmc_{stage}_{c}")
             if not os.path.isdir(d):
                 d = os.path.join(SRC, f"pmc_{c}")  # round-1 layout (batch only)
-            f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
-            v = [float(r["Counter_Value"]) for r in csv.DictReader(open(f)) if short(r["Kernel_Name"]).startswith(kname)]
-            tr[c] = sum(v) / len(v)
-            tr[c + "_dispatches"] = len(v)
-        out = {"kernel": kname, "command": f"rocprofv3 --pmc {{FETCH_SIZE|WRITE_SIZE}} --kernel-trace -- python tools/kernel_bench.py {cmd}",
+            fs = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if not fs:
+                ok = False
+                break
+            per = {}
+            for r in csv.DictReader(open(fs[0])):
+                k = short(r["Kernel_Name"])
+                if k.startswith(kname):
+                    per.setdefault(k, []).append(float(r["Counter_Value"]))
+            tr[c] = sum(sum(v) / len(v) for v in per.values())
+            tr[c + "_dispatches"] = max(len(v) for v in per.values())
+            tr["kernels"] = sorted(per)
+        if not ok:
+            continue
+        if alg is None:  # post: the spectrum in, spectrum + float64 bands + content out (bench.py post_line)
+            sys.path.insert(0, os.path.join(REPO, "audio-analyzer-omega_amd"))
+            from omega_gpu.app_post import _band_table
+            alg = 4096 * (4 * (2 * 512 + 1) + 8 * len(_band_table(48000, 2048, 512, 512)[0]))
+        out = {"kernel": " + ".join(tr["kernels"]), "command": f"rocprofv3 --pmc {{FETCH_SIZE|WRITE_SIZE}} --kernel-trace -- python tools/kernel_bench.py {cmd}",
                "fetch_size_kib": tr["FETCH_SIZE"], "write_size_kib": tr["WRITE_SIZE"],
                "traffic_bytes": 2 * tr["FETCH_SIZE"] * 1024 + tr["WRITE_SIZE"] * 1024,
                "dispatches": tr["FETCH_SIZE_dispatches"],
