@@ -230,6 +230,8 @@ struct omega_ctx {
   unsigned* h_err = nullptr;
   unsigned* d_err = nullptr;
   int poll_limit = 1 << 22;
+  float* d_lufs_scr = nullptr;  // omega_calculate_lufs: instantaneous values kept on the device
+  int64_t lufs_scr_cap = 0;
   bool res_independent = false;  // no combine target has several owners: resolution kernels commute
   hipEvent_t ev_kw = nullptr;
   struct GraphEntry {
@@ -2033,6 +2035,41 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
   }
   e = meters_enqueue(c, dl, dt, n_frames, dm, c->stream, nullptr);
   if (e) return e;
+  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+} catch (...) {
+  return guard_fail(c);
+}
+
+int omega_calculate_lufs(omega_ctx* c, const float* x, int64_t n_frames, int32_t m, int32_t mode, int32_t oversampling,
+                         float* lufs_inst, float* tp_db, double* meters, int mem) try {
+  if (!c || !x || !meters) return OMEGA_EINVAL;
+  if (n_frames <= 0) return n_frames == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
+  if (int e = check_device_err(c)) return e;
+  HIPC(c, hipSetDevice(c->device));
+  const int64_t ncf = n_frames * c->cfg.n_channels;
+  std::vector<HostOut> outs;
+  const float* dx = x;
+  float* dl = lufs_inst;
+  float* dt = tp_db;
+  double* dm = meters;
+  int e = 0;
+  if (mem == OMEGA_MEM_HOST) {
+    e = stage_in(c, 0, x, (size_t)ncf * m * sizeof(float), reinterpret_cast<const void**>(&dx));
+    if (!e) e = stage_out(c, 2, lufs_inst, ncf, outs, &dl);
+    if (!e) e = stage_out(c, 3, tp_db, ncf, outs, &dt);
+    if (!e) e = stage_out(c, 4, meters, ncf * 5, outs, &dm);
+    if (e) return e;
+  }
+  // device scratch for the instantaneous values the caller does not want back
+  if (!dl || !dt) {
+    if ((e = grow(c, &c->d_lufs_scr, &c->lufs_scr_cap, 2 * ncf))) return e;
+    if (!dl) dl = c->d_lufs_scr;
+    if (!dt) dt = c->d_lufs_scr + ncf;
+  }
+  if ((e = omega_weighting(c, dx, ncf, m, mode, nullptr, dl, OMEGA_MEM_DEVICE))) return e;
+  if ((e = omega_true_peak_os(c, dx, ncf, m, oversampling, dt, OMEGA_MEM_DEVICE))) return e;
+  if ((e = omega_meter_update(c, dl, dt, n_frames, dm, OMEGA_MEM_DEVICE))) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 } catch (...) {

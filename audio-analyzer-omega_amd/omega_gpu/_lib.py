@@ -101,6 +101,8 @@ EXPORTS = {
                                   C.c_void_p, C.c_int]),
     "omega_meter_update": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
     "omega_meter_reset": (C.c_int, [C.c_void_p]),
+    "omega_calculate_lufs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "omega_bands_create": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
                                      C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]),
     "omega_bands_destroy": (None, [C.c_void_p]),

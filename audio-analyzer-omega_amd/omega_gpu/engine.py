@@ -216,6 +216,19 @@ class Engine:
                                                out.ctypes.data, L.MEM_HOST))
         return out
 
+    def calculate_lufs(self, x: np.ndarray, mode: str = "K", oversampling: int = 4):
+        """Weighting (LUFS_inst) + true peak + meter aggregates of frames x [n_frames * C, m] in one
+        host round trip (omega_calculate_lufs). Returns (lufs_inst [n_cf], tp_db [n_cf], meters [n_cf, 5])."""
+        x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float32)
+        ncf, m = x.shape
+        li = np.empty(ncf, np.float32)
+        tp = np.empty(ncf, np.float32)
+        met = np.empty((ncf, L.N_METERS), np.float64)
+        self._check(L.lib().omega_calculate_lufs(self._ctx, x.ctypes.data, ncf // self.C, m, L.WEIGHT[mode],
+                                                 int(oversampling), li.ctypes.data, tp.ctypes.data,
+                                                 met.ctypes.data, L.MEM_HOST))
+        return li, tp, met
+
     def rfft(self, x: np.ndarray, window: str = "hann", magnitude=True, complex_out=True):
         x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float32)
         n, m = x.shape

@@ -130,9 +130,7 @@ class ProfessionalMetering:
         try:
             x = self._frame(audio_data)
             mode = "Z" if self.weighting_mode not in ("K", "A", "C") else self.weighting_mode
-            _, li = self._eng.weighting(x, mode, weighted=False)
-            tp = self._eng.true_peak(x)
-            m = self._eng.meter_update(li, tp, 1)[0]
+            m = self._eng.calculate_lufs(x, mode)[2][0]  # weighting + true peak + aggregates, one round trip
         except Exception as e:
             logger.error("calculate_lufs: %s", e)
             return self.current_lufs

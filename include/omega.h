@@ -28,6 +28,7 @@
  *   omega_drum_features    EnhancedKickDetector / EnhancedSnareDetector band flux, adaptive thresholds and
  *                          spectral centroid  omega4/analyzers/drum_detection.py:47-103, :212-305 (§8(f) row 1)
  *   omega_weighting        ProfessionalMetering.apply_weighting (K / A / C / Z) professional_meters.py:74-229
+ *   omega_calculate_lufs   ProfessionalMetering.calculate_lufs (weighting + TP + aggregates) professional_meters.py:231-281
  *                          at scipy's float64 precision, any frame length above filtfilt's padlen
  *   omega_post_*           the app's spectrum post-processing          omega4_main.py:748-1056 (§8(f) row 2)
  *   omega_vu_*             VUMetersPanel.update ballistics             omega4/panels/vu_meters.py:55-99 (§8(f) row 2)
@@ -181,6 +182,15 @@ int omega_weighting(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_
 int omega_meter_update(omega_ctx* ctx, const float* lufs_inst, const float* tp_db, int64_t n_frames,
                        double* meters, int mem);
 int omega_meter_reset(omega_ctx* ctx);
+
+/* ProfessionalMetering.calculate_lufs (professional_meters.py:231-281) in one call: weighting `mode`
+ * (LUFS_inst only, as omega_weighting), calculate_true_peak(x, oversampling) (as omega_true_peak_os)
+ * and the meter aggregates (as omega_meter_update) for n_frames x n_channels channel-frames of length
+ * m (frame-major, contiguous), with one host round trip when mem = OMEGA_MEM_HOST (the three entry
+ * points each stage, launch and synchronize on their own). lufs_inst / tp_db may be NULL (device
+ * scratch), meters [n_cf, 5] is required. */
+int omega_calculate_lufs(omega_ctx* ctx, const float* x, int64_t n_frames, int32_t m, int32_t mode,
+                         int32_t oversampling, float* lufs_inst, float* tp_db, double* meters, int mem);
 
 /* ---- band reductions (A10/A11) ---- */
 typedef struct omega_bands omega_bands;

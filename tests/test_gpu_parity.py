@@ -237,6 +237,26 @@ def test_batched_frames_match_facade(me):
     assert np.max(np.abs(out["meters"][:, 4] - g[:, 4])) < TP_TOL_DB
 
 
+def test_calculate_lufs_fused_equals_three_calls():
+    """omega_calculate_lufs (weighting + true peak + aggregates, one host round trip) gives exactly what
+    omega_weighting, omega_true_peak_os and omega_meter_update give one after the other, over a run
+    of stereo frames in every weighting mode."""
+    from omega_gpu import Engine, Resolution
+    rng = np.random.default_rng(11)
+    x = (0.2 * rng.standard_normal((40 * 2, 2048))).astype(np.float32)
+    for mode in ("K", "A", "C", "Z"):
+        kw = dict(sample_rate=FS, max_freq=20000, target_bins=2, frame_size=512, n_channels=2)
+        e1 = Engine([Resolution((20, 20000), 512, 256, 1.0)], **kw)
+        e2 = Engine([Resolution((20, 20000), 512, 256, 1.0)], **kw)
+        li, tp, met = e1.calculate_lufs(x, mode)
+        _, li2 = e2.weighting(x, mode, weighted=False)
+        tp2 = e2.true_peak(x)
+        met2 = e2.meter_update(li2, tp2, 40)
+        np.testing.assert_array_equal(li, li2)
+        np.testing.assert_array_equal(tp, tp2)
+        np.testing.assert_array_equal(met, met2)
+
+
 def test_meter_too_short_keeps_state():
     """A frame of 9 samples or fewer (scipy's filtfilt raises: padlen 9) is logged and the meters keep
     their state; 480 samples (not a power of two) is metered like the reference."""
