@@ -16,8 +16,9 @@
 // One 256-thread workgroup per frame, the float64 signal and its extension in a global working buffer
 // (L2-resident for a frame). Each lfilter pass is a chunked scan over the threads: every thread runs
 // its chunk of the 2-state recurrence s' = A s + B u from the zero state, the chunk carries are
-// combined by a Hillis-Steele scan in LDS with the powers P^(2^k) of P = A^L (computed per thread in
-// float64), and every thread re-runs its chunk from its true incoming state, writing the outputs.
+// combined by a Hillis-Steele scan with the powers P^(2^k) of P = A^L (computed per thread in
+// float64; within a wave by shuffles, across the four waves through LDS), and every thread re-runs
+// its chunk from its true incoming state, writing the outputs.
 // The outputs come from the plain recurrence (y = b0 u + z0; z0 = b1 u + z1 - a1 y; z1 = b2 u - a2 y,
 // scipy's order), so they differ from scipy's sequential lfilter only by the rounding of the
 // incoming states (~1e-16 relative).
@@ -71,21 +72,46 @@ __device__ void w64_lfilter(double* v, int n, bool rev, const W64Stage& q, doubl
   }
   double2 c = make_double2(z0, z1);
   if (t == 0) c = make_double2(c.x + (P.a * s0.x + P.b * s0.y), c.y + (P.c * s0.x + P.d * s0.y));
-  // 2) inclusive scan of the carries: c_t = sum_j P^(t-j) e_j (the initial state folded into e_0)
-  M2 Pk = P;
-  for (int d = 1; d < kW64Threads; d <<= 1) {
-    sc[t] = c;
-    __syncthreads();
-    if (t >= d) {
-      const double2 o = mvec(Pk, sc[t - d]);
-      c = make_double2(c.x + o.x, c.y + o.y);
+  // 2) inclusive scan of the carries, c_t = sum_j P^(t-j) e_j (the initial state folded into e_0):
+  // within each wave by shuffles (steps d = 1..32 with P^d; no barrier), then across the 4 waves
+  // through LDS with one barrier -- the carry into wave w, X_w, reaches lane l as P^(l+1) X_w
+  const int lane = t & 63, wv = t >> 6;
+  M2 Pd[6];  // P^(2^k)
+  Pd[0] = P;
+#pragma unroll
+  for (int k = 1; k < 6; ++k) Pd[k] = mmul(Pd[k - 1], Pd[k - 1]);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int d = 1 << k;
+    const double2 o = make_double2(__shfl_up(c.x, d, 64), __shfl_up(c.y, d, 64));
+    if (lane >= d) {
+      const double2 m = mvec(Pd[k], o);
+      c = make_double2(c.x + m.x, c.y + m.y);
     }
-    __syncthreads();
-    Pk = mmul(Pk, Pk);
   }
-  sc[t] = c;
+  if (lane == 63) sc[wv] = c;  // wave totals
   __syncthreads();
-  const double2 s = t == 0 ? s0 : sc[t - 1];
+  const M2 P64 = mmul(Pd[5], Pd[5]);
+  double2 X = make_double2(0.0, 0.0);  // carry into this wave: X_w = P^64 X_{w-1} + S_{w-1}
+  for (int v = 0; v < wv; ++v) {
+    const double2 m = mvec(P64, X);
+    X = make_double2(m.x + sc[v].x, m.y + sc[v].y);
+  }
+  // P^(l+1) by the bits of l + 1 (<= 64: P^64 for lane 63)
+  M2 Pl{1.0, 0.0, 0.0, 1.0};
+  const int e1 = lane + 1;
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    if ((e1 >> k) & 1) Pl = mmul(Pl, Pd[k]);
+  if (e1 == 64) Pl = P64;
+  {
+    const double2 m = mvec(Pl, X);
+    c = make_double2(c.x + m.x, c.y + m.y);
+  }
+  // the incoming state of this thread's chunk: the prefix of the thread before it
+  double2 s = make_double2(__shfl_up(c.x, 1, 64), __shfl_up(c.y, 1, 64));
+  if (lane == 0) s = wv == 0 ? s0 : X;
+  // (sc is next written by the following pass, after this pass's closing barrier)
   // 3) the chunk from its incoming state, outputs in place
   z0 = s.x;
   z1 = s.y;
