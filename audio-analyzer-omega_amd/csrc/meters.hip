@@ -168,7 +168,8 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   __shared__ int kp[kHistCap];                // exclusive prefix of kept flags over A (key order)
   // exclusive prefix of kept flags over B (key order); before that (rank sort) the batch's 64-bit
   // keys in time order (~0ull: not gated)
-  __shared__ __attribute__((aligned(16))) int kb[kNewCap];
+  // (+2: the rank sort's 64-bit keys K64[0..F] overlay it, F <= 1024 -- K64[F] pads the last 16-byte read)
+  __shared__ __attribute__((aligned(16))) int kb[kNewCap + 2];
   __shared__ int wsa[16], wsb[16], wsc[16];
   __shared__ double wsd[16];
   unsigned long long* K64 = reinterpret_cast<unsigned long long*>(kb);

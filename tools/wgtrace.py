@@ -18,7 +18,7 @@ from omega_gpu import _lib as _L  # noqa: E402
 
 _L.use_development_library("libomega_trace.so" if "--trace" in sys.argv else "libomega_dev.so")
 
-ROLE = {0: "kw", 1: "tp", 2: "res16k", 4: "meters", 20: "spectra", 3 + 512: "res512", 3 + 1024: "res1k", 3 + 2048: "res2k",
+ROLE = {0: "kw", 1: "tp", 2: "res16k", 4: "meters", 5: "prep", 20: "spectra", 3 + 512: "res512", 3 + 1024: "res1k", 3 + 2048: "res2k",
         3 + 4096: "res4k", 3 + 8192: "res8k"}
 
 
