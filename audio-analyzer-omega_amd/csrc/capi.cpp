@@ -230,6 +230,8 @@ struct omega_ctx {
   unsigned* h_err = nullptr;
   unsigned* d_err = nullptr;
   int poll_limit = 1 << 22;
+  unsigned long long* d_prep_u = nullptr;  // meter_prep_kernel scratch: merged keys, staged sequence
+  float* d_prep_v = nullptr;
   float* d_lufs_scr = nullptr;  // omega_calculate_lufs: instantaneous values kept on the device
   int64_t lufs_scr_cap = 0;
   bool res_independent = false;  // no combine target has several owners: resolution kernels commute
@@ -679,6 +681,8 @@ int build_meter_state(omega_ctx* c) {
   if (!e) e = dalloc(c, &c->d_next, C);
   if (!e) e = dalloc(c, &c->d_gcount, (size_t)C * (kMeterSeqCap + 1));
   if (!e) e = dalloc(c, &c->d_gsum, (size_t)C * (kMeterSeqCap + 1));
+  if (!e) e = dalloc(c, &c->d_prep_u, (size_t)C * kMeterSeqCap);
+  if (!e) e = dalloc(c, &c->d_prep_v, (size_t)C * kMeterSeqCap);
   if (!e) e = dalloc(c, &c->d_kw_done, 8);
   if (e) return e;
   if (!c->h_err) {
@@ -799,6 +803,8 @@ std::vector<MeterPrepParams> meter_chunks(omega_ctx* c, const float* lufs, const
     p.gsum = c->d_gsum;
     p.out = out + f0 * C * OMEGA_N_METERS;
     p.parts = 3;
+    p.u_scr = c->d_prep_u;
+    p.v_scr = c->d_prep_v;
     v.push_back(p);
     c->cur = b;
   }

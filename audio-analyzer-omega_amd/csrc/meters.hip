@@ -163,8 +163,12 @@ __device__ __forceinline__ void st_wt(MeterExt* q, const MeterExt& e) {
 __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   __shared__ unsigned long long B[kNewCap];   // the batch's gated keys, sorted
   __shared__ unsigned long long A[kHistCap];  // the history's gated keys, sorted
-  __shared__ unsigned long long U[kSeqCap];   // A merged with B
-  __shared__ float V[kSeqCap];                // time-ordered LUFS_inst, history ++ batch
+  // A merged with B, and the time-ordered LUFS_inst (history ++ batch), in per-channel global scratch
+  // (L2-resident): the kernel's 72 KiB of LDS then fit beside one batch workgroup (71.9 KiB) on a CU,
+  // so the prep -- resident from before the batch starts -- takes one batch slot instead of a whole
+  // CU (with 144 KiB it kept its XCD at 56 of 64 slots: tools/wgtrace.py --meters)
+  unsigned long long* U = p.u_scr + (int64_t)blockIdx.x * kSeqCap;
+  float* V = p.v_scr + (int64_t)blockIdx.x * kSeqCap;
   __shared__ int kp[kHistCap];                // exclusive prefix of kept flags over A (key order)
   // exclusive prefix of kept flags over B (key order); before that (rank sort) the batch's 64-bit
   // keys in time order (~0ull: not gated)
