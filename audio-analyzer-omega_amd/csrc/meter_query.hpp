@@ -52,6 +52,24 @@ __device__ __forceinline__ void meter_roll_tp(const MeterPrepParams& p, int c, i
   if (tid == 0) p.n_t_out[c] = ktl;
 }
 
+// The true-peak meter of output (f, c) in two parts: tp_hist_part -- the window's values from the
+// history (no dependence on this batch's true peaks, so it can run before they are counted in) -- and
+// tp_finish, the batch's values and the store (lane 0).
+__device__ __forceinline__ float tp_hist_part(const MeterPrepParams& p, int64_t f, int c, int lane) {
+  const int nt = p.n_t_in[c];
+  const int64_t ntp = nt + f + 1, wt = min<int64_t>(p.peak_len, ntp);
+  float tpm = -INFINITY;
+  for (int64_t i = ntp - wt + lane; i < nt; i += 64) tpm = fmaxf(tpm, p.hist_t_in[(int64_t)c * p.HT + i]);
+  return tpm;
+}
+__device__ __forceinline__ void tp_finish(const MeterPrepParams& p, int64_t f, int c, int lane, float tpm) {
+  const int nt = p.n_t_in[c];
+  const int64_t ntp = nt + f + 1, wt = min<int64_t>(p.peak_len, ntp);
+  for (int64_t i = max<int64_t>(ntp - wt, nt) + lane; i < ntp; i += 64) tpm = fmaxf(tpm, p.tp[(i - nt) * p.C + c]);
+  tpm = wave_max(tpm);
+  if (lane == 0) p.out[(f * p.C + c) * 5 + 4] = (double)tpm;
+}
+
 // The aggregates of output (f, c), one wave (lane = lane index): do_l the LUFS meters (columns 0-3,
 // they read the prep kernel's scratch), do_t the true-peak meter (column 4, the batch's true peaks).
 __device__ __forceinline__ void meter_query_wave(const MeterPrepParams& p, int64_t f, int c, int lane, bool do_l,

@@ -664,13 +664,20 @@ __device__ __forceinline__ void batch_meter_role(const MeterPrepParams& mp, int 
   __syncthreads();
   OMEGA_MARK(q, 1);
   for (int64_t o = o0; o < n_out; o += step) meter_query_wave(mp, o / mp.C, (int)(o % mp.C), lane, true, false);
+  // the history part of the wave's first true-peak window before the wait: after it only the batch's
+  // values are loaded (one dependent load instead of two behind the batch's last true peak)
+  const float th0 = o0 < n_out ? tp_hist_part(mp, o0 / mp.C, (int)(o0 % mp.C), lane) : -INFINITY;
   OMEGA_MARK(q, 2);
   if (tid == 0) poll_count(mp.join_ctr, mp.join_target, mp.poll_limit, mp.err_word + 1);
   __syncthreads();
   OMEGA_MARK(q, 3);
-  if (q == 0)
+  for (int64_t o = o0; o < n_out; o += step) {
+    const int64_t f = o / mp.C;
+    const int c = (int)(o % mp.C);
+    tp_finish(mp, f, c, lane, o == o0 ? th0 : tp_hist_part(mp, f, c, lane));
+  }
+  if (q == 0)  // (after the queries: they read the history this replaces in the other buffer only)
     for (int ch = 0; ch < mp.C; ++ch) meter_roll_tp(mp, ch, tid, kBatchThreads);
-  for (int64_t o = o0; o < n_out; o += step) meter_query_wave(mp, o / mp.C, (int)(o % mp.C), lane, false, true);
   OMEGA_MARK(q, 4);
 }
 
