@@ -347,6 +347,22 @@ __device__ __forceinline__ double block_sum_f(float v, double* red, int tid) {
   for (int i = 1; i < NTH / 64; ++i) r += red[i];
   return r;
 }
+// block_sum_f of v, and beside it the per-wave float sums of x in shx[NTH / 64] (same barriers)
+template <int NTH = NT>
+__device__ __forceinline__ double block_sum2_f(float v, float x, double* red, float* shx, int tid) {
+  const float w = wave_sum_sw(v);
+  const float wx = wave_sum_sw(x);
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = (double)w;
+    shx[tid >> 6] = wx;
+  }
+  __syncthreads();
+  double r = red[0];
+#pragma unroll
+  for (int i = 1; i < NTH / 64; ++i) r += red[i];
+  return r;
+}
 template <int NTH = NT>
 __device__ __forceinline__ double block_sum(double v, double* red, int tid) {
   v = wave_sum(v);

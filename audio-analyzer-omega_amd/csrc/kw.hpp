@@ -300,11 +300,15 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
   } else {
     static_for<0, L>([&](auto i) { u[i] = x[tid * L + i]; });
   }
-  // mean squares: float partials per thread (32 values) and per wave, double across waves
-  float ss = 0.f;
-  static_for<0, L>([&](auto i) { ss = fmaf(u[i], u[i], ss); });
+  // mean squares: float partials per thread (32 values) and per wave, double across waves; beside
+  // them the frame's sum (per wave in sh, across waves in float: any constant serves, see below)
+  float ss = 0.f, sx = 0.f;
+  static_for<0, L>([&](auto i) {
+    ss = fmaf(u[i], u[i], ss);
+    sx += u[i];
+  });
   OMEGA_STAMP(1);
-  const double ms_in = block_sum_f<NTH>(ss, red, tid) / M;  // (its barriers also publish pwl)
+  const double ms_in = block_sum2_f<NTH>(ss, sx, red, sh, tid) / M;  // (its barriers also publish pwl)
   OMEGA_STAMP(2);
   float* wout = p.weighted_out ? p.weighted_out + cf * M + tid * L : nullptr;
   if (p.mode == 3) {  // Z-weighting: the signal itself, no gate
@@ -318,8 +322,22 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
     if (tid == 0 && p.lufs_out) put_lufs<PUB>(p.lufs_out, cf, -100.0f);
     return;
   }
+  // Filter x - c instead of x, c = the frame's float32 mean: K(x) = K(x - c) exactly (filtfilt is
+  // linear; both sections are high-passes, b sums to 0, and the odd extension and the lfilter_zi
+  // initial states hold a constant at its steady state, whose response is 0 -- checked on the oracle,
+  // tests/test_oracle_golden.py). On DC-biased frames (the capture path removes no DC) the float32
+  // state otherwise carries the offset, and its rounding, amplified ~300x by the high-pass poles,
+  // reaches 0.1 LU at 0.9 DC + 1e-4 noise. x - c is exact where c and x are within a factor 2 of each
+  // other (Sterbenz) and otherwise rounded to the result's own ulp.
+  {
+    float c = 0.f;
+#pragma unroll
+    for (int w = 0; w < NTH / 64; ++w) c += sh[w];
+    c *= 1.0f / M;
+    static_for<0, L>([&](auto i) { u[i] -= c; });
+  }
   gather_edges<L, NTH, OPQ>(u, edge, tid);
-  __syncthreads();
+  __syncthreads();  // (sh, read above, is the scan's scratch after this barrier)
   OMEGA_STAMP(3);
   filtfilt<L, NTH, 4, OPQ>(u, p.hp, pwl[0], edge, sh, tid);
   // u = f (high-passed): park it in LDS, run the shelf stage on u

@@ -208,6 +208,17 @@ class Engine:
     def k_weighting(self, x: np.ndarray, weighted: bool = True):
         return self.weighting(x, "K", weighted)
 
+    def k_weighting_scan(self, x: np.ndarray, weighted: bool = True):
+        """The batch path's float32 chunked-scan K-weighting on its own (omega_k_weighting,
+        kweight_kernel: power-of-two frames 512..16384) -- what omega_process_frames computes LUFS_inst
+        with; ``k_weighting`` / ``weighting`` run scipy's float64 cascade instead."""
+        x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float32)
+        w = np.empty_like(x) if weighted else None
+        li = np.empty(x.shape[0], np.float32)
+        self._check(L.lib().omega_k_weighting(self._ctx, x.ctypes.data, x.shape[0], x.shape[1],
+                                              w.ctypes.data if w is not None else None, li.ctypes.data, L.MEM_HOST))
+        return w, li
+
     def meter_update(self, lufs_inst, tp_db, n_frames: int) -> np.ndarray:
         li = np.ascontiguousarray(lufs_inst, dtype=np.float32)
         tp = np.ascontiguousarray(tp_db, dtype=np.float32)

@@ -64,6 +64,16 @@ class ProfessionalMetering:
     def _frame(audio_data):
         return np.asarray(audio_data, dtype=np.float32).ravel()
 
+    @staticmethod
+    def _tp_type(audio_data):
+        """The dtype calculate_true_peak returns (professional_meters.py:289-299): scipy's resample
+        keeps float32 (and computes float16 in float32) and gives float64 for every other input, int
+        frames and lists included; ``20 * np.log10`` keeps that type. Silence is the Python float
+        -100.0 the reference returns (:295-296)."""
+        dt = np.asarray(audio_data).dtype
+        t = np.float32 if dt in (np.float32, np.float16) else np.float64
+        return lambda v: -100.0 if v == -100.0 else t(v)
+
     def apply_k_weighting(self, audio_data: np.ndarray) -> np.ndarray:
         """professional_meters.py:129-153 (returned as float64 like scipy's filtfilt)."""
         return self._weighted(audio_data, "K")
@@ -114,11 +124,13 @@ class ProfessionalMetering:
         return self._weighted(audio_data, self.weighting_mode)
 
     def calculate_true_peak(self, audio_data: np.ndarray, oversampling: int = 4) -> float:
-        """professional_meters.py:283-299 (float32 result for float32 input, like scipy)."""
+        """professional_meters.py:283-299 (the result follows the input dtype like scipy's resample:
+        float32 for float32 frames, float64 for the app's float64 Hann frames, omega4_main.py:1082)."""
         if len(audio_data) == 0:
             return -100.0
         try:
-            self.current_true_peak = np.float32(self._eng.true_peak(self._frame(audio_data), oversampling)[0])
+            tp = self._eng.true_peak(self._frame(audio_data), oversampling)[0]
+            self.current_true_peak = self._tp_type(audio_data)(tp)
         except Exception as e:
             logger.error("calculate_true_peak: %s", e)
         return self.current_true_peak
@@ -138,7 +150,7 @@ class ProfessionalMetering:
         self.current_lufs["short_term"] = np.float64(m[1])
         self.current_lufs["integrated"] = np.float64(m[2])
         self.current_lufs["range"] = np.float64(m[3])
-        self.current_lufs["true_peak"] = np.float32(m[4])
+        self.current_lufs["true_peak"] = self._tp_type(audio_data)(m[4])
         return self.current_lufs
 
     def calculate_lufs_batch(self, frames: np.ndarray) -> np.ndarray:

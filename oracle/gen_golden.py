@@ -753,11 +753,28 @@ def gen_post_threshold(R):
     np.savez_compressed(path, **g)
 
 
+def gen_meters_dc(R):
+    """The reference's own calculate_lufs / apply_weighting / calculate_true_peak on DC-offset frames
+    (SURVEY §8(a) A6-A9); also the float64 Hann-windowed form the app feeds the panel."""
+    d = {"versions": VERSIONS}
+    for name, fr in S.dc_meter_frames().items():
+        li, tp, agg = _meter_run(R, fr)
+        d[f"{name}/lufs_inst"], d[f"{name}/tp"], d[f"{name}/agg"] = li, tp, agg
+    h = np.hanning(16384)
+    fr64 = S.dc_meter_frames()["dc05_n1e3"].astype(np.float64) * h
+    li, tp, agg = _meter_run(R, fr64)
+    d["hann64_dc05/lufs_inst"], d["hann64_dc05/tp"], d["hann64_dc05/agg"] = li, tp, agg
+    d["hann64_dc05/tp_dtype"] = np.array(str(np.asarray(R.ProfessionalMetering(FS).calculate_true_peak(fr64[0])).dtype))
+    d["dc09_n1e4/tp_dtype"] = np.array(str(np.asarray(R.ProfessionalMetering(FS).calculate_true_peak(
+        S.dc_meter_frames()["dc09_n1e4"][0])).dtype))
+    np.savez_compressed(os.path.join(OUT, "meters_dc.npz"), **d)
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference not present: golden vectors can only be generated in the build container")
     os.makedirs(OUT, exist_ok=True)
     R = _import_reference()
-    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac", "meters_any", "mrfft_small", "transients_any", "post_ema", "post_threshold", "capture_stereo"))]:
+    for g in [globals()[f"gen_{n}"] for n in (sys.argv[1:] or ("mrfft", "meters", "bands", "chroma", "batched", "drums", "post", "chroma_genre", "gpufft", "capture", "vu", "transients", "weighting_ac", "meters_any", "mrfft_small", "transients_any", "post_ema", "post_threshold", "capture_stereo", "meters_dc"))]:
         g(R)
         print("wrote", g.__name__)

@@ -84,3 +84,25 @@ def cfg5_stream(n: int, channels: int = 8, fs: float = 96000) -> np.ndarray:
     t = np.arange(n) / fs
     return np.stack([(0.2 * np.sin(2 * np.pi * 110 * (c + 1) * t)).astype(np.float32) + noise(c, n, 0.02)
                      for c in range(channels)]).astype(np.float32)
+
+
+def dc_meter_frames(n: int = 8, m: int = 16384) -> dict:
+    """DC-biased 16384-sample meter frames (the capture path passes raw samples with no DC removal,
+    capture.py:571-574, :620-641): large constant offsets under low-level content, where a float32
+    IIR's state rounding at the DC level is amplified by the high-pass poles (radius ~0.9965).
+    Returns {name: f32[n, m]}; ``hann_dc05`` is the app's Hann-windowed form (omega4_main.py:1082)
+    rounded to float32 (its float64 product is ``dc05_n1e3 * np.hanning(m)``)."""
+    t = np.arange(n * m)
+    rng = np.random.default_rng(77)
+    seqs = {
+        "dc09_n1e4": 0.9 + 1e-4 * rng.standard_normal(n * m),
+        "dc05_n1e3": 0.5 + 1e-3 * rng.standard_normal(n * m),
+        "dcm07_n3e4": -0.7 + 3e-4 * rng.standard_normal(n * m),
+        "dc03_sine": 0.3 + 0.25 * np.sin(2 * np.pi * 997 * t / FS) + 1e-3 * rng.standard_normal(n * m),
+        "dc09_sine1e3": 0.9 + 1e-3 * np.sin(2 * np.pi * 60 * t / FS),
+        # a step of the offset inside frame 3
+        "dc_step": np.where(t < 3 * m + 5000, 0.2, 0.8) + 2e-4 * rng.standard_normal(n * m),
+    }
+    out = {k: v.astype(np.float32).reshape(n, m) for k, v in seqs.items()}
+    out["hann_dc05"] = (out["dc05_n1e3"].astype(np.float64) * np.hanning(m)).astype(np.float32)
+    return out

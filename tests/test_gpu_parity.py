@@ -171,7 +171,7 @@ def test_meter_instantaneous(me, name):
     from omega_gpu import Engine, Resolution
     frames = me[f"{name}/x"]
     e = Engine([Resolution((20, 20000), 512, 256, 1.0)], FS, 20000, 2, frame_size=512)
-    _, li = e.k_weighting(frames, weighted=False)  # the batch kernel's float32 scan
+    _, li = e.k_weighting_scan(frames, weighted=False)  # the batch kernel's float32 scan
     np.testing.assert_allclose(li, me[f"{name}/lufs_inst"], rtol=0, atol=LU_TOL)
     tp = e.true_peak(frames)
     np.testing.assert_allclose(tp, me[f"{name}/tp"], rtol=0, atol=TP_TOL_DB)
@@ -179,6 +179,67 @@ def test_meter_instantaneous(me, name):
     assert np.max(np.abs(li - me[f"{name}/lufs_inst"])) < 0.01
     _, li64 = e.weighting(frames, "K", weighted=False)  # omega_weighting: scipy's float64 filtfilt
     assert np.max(np.abs(li64 - me[f"{name}/lufs_inst"])) < 1e-4
+
+
+DC_SEQS = ["dc09_n1e4", "dc05_n1e3", "dcm07_n3e4", "dc03_sine", "dc09_sine1e3", "dc_step", "hann_dc05"]
+
+
+@pytest.fixture(scope="module")
+def mdc():
+    return load_golden("meters_dc")
+
+
+@pytest.mark.parametrize("name", DC_SEQS)
+def test_meter_dc_offset_batch_path(mdc, name):
+    """DC-biased 16384-sample frames (capture passes raw samples, capture.py:571-574) through the
+    cfg2 batch launch (float32 K-weighting scan, true peak, meter aggregates) and the standalone
+    float32 K-weighting kernel, against the reference's own calculate_lufs on the same frames
+    (tests/golden/meters_dc.npz). A float32 direct-form filtfilt is ~0.1 LU off at 0.9 DC + 1e-4
+    noise -- this scan was 6.09 LU off on dc09_n1e4, 0.91 on dcm07_n3e4 and 2.28 on dc_step (MI355X,
+    round 4) before it filtered x - mean(x) (K(x) = K(x - c) exactly: both sections are high-passes
+    with odd extension and lfilter_zi initial states); now <= 0.003 LU on the constant offsets. The
+    Hann-windowed offset is not a constant and keeps 0.015 LU (0.044 before). Bars: 0.01 LU for the
+    constant offsets, 0.03 for the Hann form (the north star's is 0.1)."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS, Resolution
+    fr = S.dc_meter_frames()[name]
+    n = len(fr)
+    eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=1)
+    out = eng.process_frames(torch.from_numpy(fr).cuda(), n, 16384, 16384, meters=True)
+    torch.cuda.synchronize()
+    out = {k: v.cpu().numpy() for k, v in out.items()}
+    bar = 0.03 if name.startswith("hann") else 0.01
+    li_err = np.abs(out["lufs_inst"] - mdc[f"{name}/lufs_inst"])
+    assert li_err.max() < bar, li_err
+    assert np.abs(out["true_peak_db"] - mdc[f"{name}/tp"]).max() < TP_TOL_DB
+    agg = mdc[f"{name}/agg"]
+    assert np.abs(out["meters"][:, :4] - agg[:, :4]).max() < bar
+    assert np.abs(out["meters"][:, 4] - agg[:, 4]).max() < TP_TOL_DB
+    e = Engine([Resolution((20, 20000), 512, 256, 1.0)], FS, 20000, 2, frame_size=512)
+    _, li = e.k_weighting_scan(fr, weighted=False)  # kweight_kernel: the same scan standalone
+    assert np.abs(li - mdc[f"{name}/lufs_inst"]).max() < bar
+    _, li64 = e.k_weighting(fr, weighted=False)  # omega_weighting: scipy's float64 cascade
+    assert np.abs(li64 - mdc[f"{name}/lufs_inst"]).max() < 1e-4
+
+
+def test_meter_dc_offset_facade_float64(mdc):
+    """The app's call: float64 Hann-windowed frames into calculate_lufs / calculate_true_peak
+    (omega4_main.py:1082). Values against the reference's, and the true peak's type follows the input
+    like scipy's resample (professional_meters.py:289-299): float64 here, float32 for float32 frames."""
+    from omega_gpu.professional_meters import ProfessionalMetering
+    fr64 = S.dc_meter_frames()["dc05_n1e3"].astype(np.float64) * np.hanning(16384)
+    pm = ProfessionalMetering(FS)
+    agg = mdc["hann64_dc05/agg"]
+    for f, x in enumerate(fr64):
+        d = pm.calculate_lufs(x)
+        got = np.array([d[k] for k in ("momentary", "short_term", "integrated", "range", "true_peak")])
+        assert np.abs(got[:4] - agg[f, :4]).max() < 0.01, (f, got, agg[f])
+        assert abs(got[4] - agg[f, 4]) < TP_TOL_DB
+        assert type(d["true_peak"]) is np.float64 and type(d["integrated"]) is np.float64
+    assert str(mdc["hann64_dc05/tp_dtype"]) == "float64" and str(mdc["dc09_n1e4/tp_dtype"]) == "float32"
+    assert type(pm.calculate_true_peak(fr64[0])) is np.float64
+    assert type(pm.calculate_true_peak(fr64[0].astype(np.float32))) is np.float32
+    assert type(pm.calculate_true_peak(np.zeros(2048))) is float
 
 
 def test_meter_long_window_batch(me):

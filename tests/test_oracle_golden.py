@@ -185,6 +185,34 @@ def test_meter_sequences(me, name):
     np.testing.assert_allclose(agg, me[f"{name}/agg"], rtol=0, atol=1e-5)
 
 
+@pytest.mark.parametrize("name", ["dc09_n1e4", "dc05_n1e3", "dcm07_n3e4", "dc03_sine", "dc09_sine1e3", "dc_step",
+                                  "hann_dc05"])
+def test_meter_dc_offset_oracle(name):
+    """DC-biased frames (tests/golden/meters_dc.npz, the reference's calculate_lufs): the oracle, and
+    the identity the batch kernel's float32 scan relies on -- K(x) = K(x - c) for any constant c
+    (filtfilt is linear; both sections are high-passes, b sums to 0, and the odd extension and the
+    lfilter_zi initial states keep a constant at its steady state, whose response is 0)."""
+    g = load_golden("meters_dc")
+    fr = S.dc_meter_frames()[name]
+    li, tp, agg = R.meter_sequence(fr, FS)
+    np.testing.assert_allclose(li, g[f"{name}/lufs_inst"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(tp, g[f"{name}/tp"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(agg[:, :4], g[f"{name}/agg"][:, :4], rtol=0, atol=1e-9)
+    for x in fr[:3].astype(np.float64):
+        y0 = R.apply_k_weighting(x, FS)
+        for c in (np.mean(x), np.float32(np.mean(x)), x[0], 0.37):
+            y1 = R.apply_k_weighting(x - c, FS)
+            assert np.max(np.abs(y1 - y0)) < 1e-9 * max(1.0, np.max(np.abs(x))), (c, np.max(np.abs(y1 - y0)))
+
+
+def test_meter_dc_offset_float64_app_form():
+    g = load_golden("meters_dc")
+    fr64 = S.dc_meter_frames()["dc05_n1e3"].astype(np.float64) * np.hanning(16384)
+    li, tp, agg = R.meter_sequence(fr64, FS)
+    np.testing.assert_allclose(li, g["hann64_dc05/lufs_inst"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(agg[:, :4], g["hann64_dc05/agg"][:, :4], rtol=0, atol=1e-9)
+
+
 def test_meter_long_window(me):
     """3700 frames: the 3600-deep integrated deque evicts (professional_meters.py:22)."""
     li, tp, agg = R.meter_sequence(S.level_steps(3700, 512, seed=9), FS)
