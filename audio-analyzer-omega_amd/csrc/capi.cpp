@@ -61,9 +61,11 @@ constexpr double kPi = 3.14159265358979323846;
 constexpr int kChunkFrames = kMeterChunk;
 constexpr int kBatchWaves = 8;  // waves of a batch_kernel workgroup (rfkern.hip kBatchThreads / 64)
 // meter workgroups of the batch grid at most: they wait (spinning) for the meter prep kernel, which
-// needs a whole CU's LDS, so they must never fill every CU (MI355X: 256 CUs, 2 batch slots each; a
-// 4096-frame batch with one meter workgroup per 8 outputs took all 512 slots and waited until the
-// poll bound expired)
+// may be dispatched after them and needs a CU with at most one batch workgroup resident (1024 threads
+// and 72.6 KiB of LDS beside one 512-thread, 71.9 KiB batch workgroup). 64 waiting workgroups hold at
+// most 64 of the 512 batch slots, so at least 192 CUs keep a slot that other roles free as they
+// finish. (Round 1: one meter workgroup per 8 outputs of a 4096-frame batch took every slot and waited
+// until the poll bound expired.)
 constexpr int kMeterWgs = 64;
 
 struct DevBuf {
@@ -208,7 +210,7 @@ struct omega_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
   // fork/join streams + events for the concurrent branches, and the graph cache
-  hipStream_t cap = nullptr, fork[2] = {nullptr, nullptr};
+  hipStream_t cap = nullptr, fork[1] = {nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   // HIP graph replay of device-memory calls: off by default -- on MI355X (ROCm 7) a replayed graph
   // put the stream layout's nodes on other queues, with ~12 us cross-queue waits and ~20 us between
@@ -752,10 +754,28 @@ int stage_out(omega_ctx* c, int slot, T* host, size_t count, std::vector<HostOut
   return 0;
 }
 
+// A device-side ordering wait that expired (meters.hip: the prep kernel's wait for the batch's
+// K-weighting count, the join of the LUFS meters into the caller's stream) means some meter aggregates
+// were computed from, or returned before, incomplete inputs: report it once as OMEGA_EHIP.
+int check_device_err(omega_ctx* c) {
+  if (!c->h_err) return 0;
+  volatile unsigned* e = c->h_err;
+  const unsigned prep = e[0], join = e[1];
+  if (!prep && !join) return 0;
+  e[0] = 0;
+  e[1] = 0;
+  return fail(c, OMEGA_EHIP, "device-side meter ordering wait expired (%s%s%s): meter aggregates of an earlier call "
+              "may be stale", prep ? "meter prep waiting for the K-weighting count" : "", prep && join ? ", " : "",
+              join ? "caller's stream joining the LUFS meters" : "");
+}
+
+// Host-memory calls: copy the outputs back and wait; an ordering wait of THIS call that expired is
+// reported by this call (device-memory calls report it at the next call or omega_synchronize).
 int finish_host(omega_ctx* c, const std::vector<HostOut>& outs) {
   for (const HostOut& o : outs) HIPC(c, hipMemcpyAsync(o.host, o.dev, o.bytes, hipMemcpyDeviceToHost, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
-  return 0;
+  if (c->fork[0]) HIPC(c, hipStreamSynchronize(c->fork[0]));
+  return check_device_err(c);
 }
 
 // Meter aggregates over n_frames x C values, in chunks of at most kChunkFrames frames; each chunk
@@ -832,7 +852,7 @@ int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_f
 bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, bool do_res, hipStream_t s,
                     int* mr) {
   *mr = -1;
-  if (W != 16384 || s == c->cap) return false;
+  if (W != 16384 || (c->cap && s == c->cap)) return false;  // (graph capture: the other layout)
   if ((kp.lufs_out || kp.weighted_out) && kp.mode != 0) return false;
   if (!do_res) return true;
   if (!c->res_independent) return false;
@@ -1016,7 +1036,7 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
 
 extern "C" {
 
-const char* omega_version(void) { return "omega-mi355x 0.1 (gfx950, ABI 1)"; }
+const char* omega_version(void) { return "omega-mi355x 0.2 (gfx950, ABI 2)"; }
 
 #ifdef OMEGA_STAMPS
 // Development build only (make dev): one kernel variant over n_cf channel-frames of the context's
@@ -1096,7 +1116,8 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) try {
   // the one environment variable the library reads: the device-wait bound of the meter ordering
   // (a test knob: tests/test_gpu_parity.py test_meter_ordering_expiry_is_reported)
   if (const char* pl = std::getenv("OMEGA_POLL_LIMIT")) c->poll_limit = std::atoi(pl) > 0 ? std::atoi(pl) : 1;
-  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking);
+  // (the graph-capture stream is created on the first capture: a context holds two streams --
+  // the hardware has GPU_MAX_HW_QUEUES = 4 queues per process, see omega.h on the meter ordering)
   if (he == hipSuccess) {
     // fork[0] carries the latency-bound meter kernels beside full-chip work: at the highest stream
     // priority a freed CU goes to them first
@@ -1106,7 +1127,6 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) try {
     else
       he = hipStreamCreateWithFlags(&c->fork[0], hipStreamNonBlocking);
   }
-  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->fork[1], hipStreamNonBlocking);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_join[0], hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_join[1], hipEventDisableTiming);
@@ -1525,10 +1545,10 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   p.band_out = bands_out;
   p.content_out = content_out;
   // scratch: the raw band rows (+ the EMA's spare rows: post.hip post_ema_kernel), the per-frame dtype
-  // flags, then (8-byte aligned) the EMA chunks' warm-up values at their boundaries, end values and
-  // boundary mismatch flags
+  // flags, then (16-byte aligned) the EMA chunks' warm-up values at their boundaries, end values and
+  // boundary mismatch flags (post_ema_fix_kernel reads the flags as 16-byte vectors)
   const int64_t rows = n_frames + kEmaSpareRows, nch = (n_frames + 63) / 64;
-  const int64_t pre_off = (rows * (c->post.nb + 1) + 1) / 2 * 2;
+  const int64_t pre_off = (rows * (c->post.nb + 1) + 3) / 4 * 4;
   const int64_t nchp = (nch + 15) / 16 * 16;
   if (c->post.nb) {
     if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, pre_off + 4 * nch * c->post.nb + nchp * c->post.nb / 4 + 4))
@@ -1539,6 +1559,8 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   p.ema_pre = reinterpret_cast<double*>(c->d_post_raw + pre_off);
   p.ema_end = p.ema_pre + nch * c->post.nb;
   p.ema_flag = reinterpret_cast<unsigned char*>(p.ema_end + nch * c->post.nb);
+  if (reinterpret_cast<uintptr_t>(p.ema_flag) % 16 != 0)
+    return fail(c, OMEGA_EHIP, "post scratch: EMA flags not 16-byte aligned");
   HIPC(c, launch_post(p, c->stream));
   if (c->post.nb) {  // the EMA wrote the other state buffer: it is the next call's input
     std::swap(c->post.prev, c->post.prev_out);
@@ -1547,21 +1569,6 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   return 0;
 } catch (...) {
   return guard_fail(c);
-}
-
-// A device-side ordering wait that expired (meters.hip: the prep kernel's wait for the batch's
-// K-weighting count, the join of the LUFS meters into the caller's stream) means some meter aggregates
-// were computed from, or returned before, incomplete inputs: report it once as OMEGA_EHIP.
-int check_device_err(omega_ctx* c) {
-  if (!c->h_err) return 0;
-  volatile unsigned* e = c->h_err;
-  const unsigned prep = e[0], join = e[1];
-  if (!prep && !join) return 0;
-  e[0] = 0;
-  e[1] = 0;
-  return fail(c, OMEGA_EHIP, "device-side meter ordering wait expired (%s%s%s): meter aggregates of an earlier call "
-              "may be stale", prep ? "meter prep waiting for the K-weighting count" : "", prep && join ? ", " : "",
-              join ? "caller's stream joining the LUFS meters" : "");
 }
 
 void omega_destroy(omega_ctx* c) try {
@@ -1578,7 +1585,7 @@ void omega_destroy(omega_ctx* c) try {
     if (b.p) (void)hipFree(b.p);
   drop_graphs(c);
   if (c->h_err) (void)hipHostFree(c->h_err);
-  for (hipStream_t st : {c->cap, c->fork[0], c->fork[1]})
+  for (hipStream_t st : {c->cap, c->fork[0]})
     if (st) (void)hipStreamDestroy(st);
   for (hipEvent_t ev : {c->ev_fork, c->ev_join[0], c->ev_join[1], c->ev_kw})
     if (ev) (void)hipEventDestroy(ev);
@@ -1591,7 +1598,19 @@ const char* omega_last_error(const omega_ctx* c) { return c ? c->err : "null con
 
 int omega_set_stream(omega_ctx* c, void* s) try {
   if (!c) return OMEGA_EINVAL;
-  c->stream = static_cast<hipStream_t>(s);  // NULL = the null (default) stream, e.g. torch's default
+  const hipStream_t ns = static_cast<hipStream_t>(s);  // NULL = the null (default) stream, e.g. torch's
+  if (ns != c->stream) {
+    // The work already enqueued on the old stream -- a batch's meter segment still reading the
+    // per-context prep scratch and history, a query kernel -- must finish before the next call's work:
+    // on one stream that is stream order, and the next meter prep on fork[0] waits for the next
+    // batch's K-weighting count, i.e. for a batch that started after the previous one ended. Across a
+    // stream switch nothing orders them, so the new stream and fork[0] wait once for the old stream.
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPC(c, hipStreamWaitEvent(ns, c->ev_fork, 0));
+    HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
+    c->stream = ns;
+  }
   return 0;
 } catch (...) {
   return guard_fail(c);
@@ -1719,6 +1738,7 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
         c->graphs.clear();
       }
       const int cur0 = c->cur;
+      if (!c->cap) HIPC(c, hipStreamCreateWithFlags(&c->cap, hipStreamNonBlocking));
       HIPC(c, hipStreamBeginCapture(c->cap, hipStreamCaptureModeThreadLocal));
       e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->cap);
       hipGraph_t graph = nullptr;

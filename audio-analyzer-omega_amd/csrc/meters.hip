@@ -434,7 +434,14 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
   OMEGA_MARK(c, 2);
   if (p.q_done) {
     // count this channel's prep in for the batch's meter segment: every wave's (write-through) stores
-    // drained, then a relaxed add
+    // drained, then a relaxed add. INVARIANT: every field the in-grid queries (meter_query.hpp) read
+    // is stored above with st_wt (write-through, agent scope): core[], ext[], gp[] (time-order gated
+    // prefix counts), gsum[] (their sums), n_core[c], n_ext[c]; the LUFS history, its count and the
+    // next frame index (hist_l_out, n_l_out, n_s_out, t0_out) are read only by the NEXT batch's prep and
+    // queries, which run behind the next prep, itself ordered behind this kernel on fork[0]. A plain store to one of the former would reach the
+    // query on another XCD late, without any warning: there is no release here for the query's poll to
+    // synchronise with -- the ordering rests on sc1 stores being acknowledged once coherent across
+    // XCDs, then this vmcnt drain.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(p.q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -653,8 +653,8 @@ __device__ __forceinline__ void batch_kw_role(const KWeightParams& kp, int64_t c
 // batch's K-weighting count), then the LUFS meters; then until every true-peak workgroup has counted
 // in, then the true-peak meter (workgroup 0 also rolls the true-peak history). The batch completes only
 // after both, so the caller's stream needs no join kernel and no stream event. nq is at most
-// kMeterWgs (the host's cap): the waiting workgroups must leave CUs free for the prep kernel, which
-// needs a whole CU's LDS and may be dispatched after them.
+// kMeterWgs (the host's cap): the waiting workgroups must leave room for the prep kernel, which may be
+// dispatched after them and needs a CU with at most one batch workgroup resident (capi.cpp kMeterWgs).
 __device__ __forceinline__ void batch_meter_role(const MeterPrepParams& mp, int q, int nq, int tid) {
   const int64_t n_out = mp.n_frames * mp.C, step = (int64_t)nq * (kBatchThreads / 64);
   const int64_t o0 = (int64_t)q * (kBatchThreads / 64) + (tid >> 6);

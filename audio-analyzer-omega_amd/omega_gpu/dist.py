@@ -1,7 +1,9 @@
 """Multi-GPU layout for the per-frame path: one process per GPU, channel-frames
-sharded in contiguous blocks of the batch axis (weak scaling: every rank owns whole streams, so the
-meter aggregates need no exchange), and each rank's per-frame outputs gathered to rank 0 over RCCL
-(backend "nccl") -- the only collective, overlapped with the next batch by the caller.
+sharded in contiguous blocks of the batch axis (weak scaling), and each rank's per-frame outputs
+gathered to rank 0 over RCCL (backend "nccl"), overlapped with the next batch by the caller. Two
+stream layouts: every rank owns whole streams (bench.py: one independent stream per rank, the meter
+aggregates need no exchange), or one stream's frames are split over the ranks in time
+(TimeShardExchange below: the meters' history is all-gathered before the local meter update).
 
 Packed block of one rank (PackedLayout): ONE flat byte buffer holding the outputs planar, so the
 engine writes straight into it (the output dict is a set of views) and the gather moves it as it is,
@@ -83,3 +85,94 @@ def unpack_gathered(recv: List[torch.Tensor], layout: PackedLayout) -> Dict[str,
     """Rank 0: the gathered blocks as one output dict in global channel-frame order (rank-major)."""
     vs = [layout.views(b) for b in recv]
     return {k: torch.cat([v[k] for v in vs]) for k in vs[0]}
+
+
+# ---- time-sharded streams: the meter aggregates' history exchange (SURVEY.md §8(e)) ----
+#
+# When one stream's consecutive frames are split over the ranks (rank r holds frames [a_r, b_r) of the
+# same stream, for every channel), the aggregates of a frame read the LUFS_inst of the 3599 frames
+# before it and the true peaks of the 59 before it (the deques of professional_meters.py:20-25, used
+# at :249-279) -- frames other ranks computed. Per global batch every rank (1) computes its shard's
+# LUFS_inst and true peaks (the batch launch without meters), (2) all-gathers its shard's last 3599 /
+# 59 values (~30 KB per channel), (3) loads the stream's history before a_r into its meter state (reset,
+# then the history fed through omega_meter_update with its outputs discarded: the device state ends
+# exactly as if it had metered those frames) and (4) meters its shard. The tails of all ranks also
+# carry the stream into the next global batch. The result equals one context metering the whole
+# stream, bitwise (tests/test_dist.py over gloo, tests/test_gpu_parity.py on the device).
+
+LUFS_HIST = 3599  # the 3600-deep integrated deque minus the frame itself
+TP_HIST = 59      # the 60-deep peak-hold deque minus the frame itself
+
+
+def stream_history(prev_li: torch.Tensor, prev_tp: torch.Tensor, tails: List[Tuple[torch.Tensor, torch.Tensor]],
+                   upto: int, nl: int = LUFS_HIST, nt: int = TP_HIST) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The stream's last nl LUFS_inst / nt true-peak rows before shard `upto` of this global batch:
+    prev (the stream before the batch) ++ the tails of shards 0..upto-1, cut to the last nl / nt rows.
+    Each tail holds the last <= nl / nt rows of its shard, so nothing earlier than a cut tail is needed."""
+    li = torch.cat([prev_li] + [t[0] for t in tails[:upto]])[-nl:] if nl > 0 else prev_li[:0]
+    tp = torch.cat([prev_tp] + [t[1] for t in tails[:upto]])[-nt:] if nt > 0 else prev_tp[:0]
+    return li, tp
+
+
+def history_frames(li: torch.Tensor, tp: torch.Tensor, fill: float = -100.0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """LUFS_inst / true-peak rows to feed through the meter update as pseudo-frames: one frame per
+    LUFS row, the true peaks aligned to the last rows (older frames get `fill`: they leave the 60-deep
+    peak hold before any real frame is metered)."""
+    n = li.shape[0]
+    full = torch.full_like(li, fill)
+    k = min(n, tp.shape[0])
+    if k:
+        full[n - k:] = tp[tp.shape[0] - k:]
+    return li, full
+
+
+class TimeShardExchange:
+    """Per-rank carrier of the stream history across global batches for a time-sharded stream of C
+    channels (rows = frames, columns = channels; float32 like the device's LUFS_inst / true peaks)."""
+
+    def __init__(self, channels: int, device=None, nl: int = LUFS_HIST, nt: int = TP_HIST):
+        self.C, self.nl, self.nt = int(channels), int(nl), int(nt)
+        self.prev_li = torch.empty(0, self.C, dtype=torch.float32, device=device)
+        self.prev_tp = torch.empty(0, self.C, dtype=torch.float32, device=device)
+
+    def _block(self, li: torch.Tensor, tp: torch.Tensor) -> torch.Tensor:
+        """Fixed-size message: nl LUFS rows, nt true-peak rows, two count rows (all_gather needs equal
+        sizes; a shard shorter than nl / nt sends fewer rows)."""
+        blk = torch.zeros(self.nl + self.nt + 2, self.C, dtype=torch.float32, device=li.device)
+        tl, tt = li[-self.nl:] if self.nl else li[:0], tp[-self.nt:] if self.nt else tp[:0]
+        blk[:tl.shape[0]] = tl
+        blk[self.nl:self.nl + tt.shape[0]] = tt
+        blk[-2, 0], blk[-1, 0] = float(tl.shape[0]), float(tt.shape[0])
+        return blk
+
+    def _unblock(self, blk: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        cnt = blk[-2:, 0].cpu()
+        nl, nt = int(cnt[0]), int(cnt[1])
+        return blk[:nl], blk[self.nl:self.nl + nt]
+
+    def exchange(self, li: torch.Tensor, tp: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """li, tp: this rank's shard [n, C] in time order. All-gathers every rank's tail and returns the
+        stream's history before this rank's first frame (LUFS rows, true-peak rows); advances the
+        carried history past the whole global batch."""
+        import torch.distributed as dist
+        if li.dim() != 2 or li.shape[1] != self.C or tp.shape != li.shape:
+            raise ValueError(f"shard values must be [n, {self.C}] (LUFS_inst and true peak alike)")
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        blk = self._block(li, tp)
+        got = [torch.empty_like(blk) for _ in range(world)]
+        dist.all_gather(got, blk, group=group)
+        tails = [self._unblock(b) for b in got]
+        hist = stream_history(self.prev_li, self.prev_tp, tails, rank, self.nl, self.nt)
+        self.prev_li, self.prev_tp = stream_history(self.prev_li, self.prev_tp, tails, world, self.nl, self.nt)
+        return hist
+
+
+def meter_time_shard(engine, li: torch.Tensor, tp: torch.Tensor, hist: Tuple[torch.Tensor, torch.Tensor]):
+    """Step (3)-(4) on one rank: load the exchanged history into the engine's meter state, then meter
+    the shard. `engine` offers reset_meters() and meter_update(li, tp, n_frames) over [n, C] rows
+    (omega_gpu.Engine on the device). Returns the shard's meters [n * C, 5]."""
+    engine.reset_meters()
+    hl, ht = history_frames(*hist)
+    if hl.shape[0]:
+        engine.meter_update(hl.contiguous(), ht.contiguous(), hl.shape[0])
+    return engine.meter_update(li.contiguous(), tp.contiguous(), li.shape[0])

@@ -219,7 +219,20 @@ class Engine:
                                               w.ctypes.data if w is not None else None, li.ctypes.data, L.MEM_HOST))
         return w, li
 
-    def meter_update(self, lufs_inst, tp_db, n_frames: int) -> np.ndarray:
+    def meter_update(self, lufs_inst, tp_db, n_frames: int):
+        """The A9 aggregates of n_frames x C injected (LUFS_inst, true peak) values in frame order
+        (host numpy, or device torch float32 tensors: then the result is a device tensor too)."""
+        if _is_torch(lufs_inst):
+            import torch
+            li, tp = lufs_inst.contiguous(), tp_db.contiguous()
+            if li.dtype != torch.float32 or tp.dtype != torch.float32 or li.numel() != n_frames * self.C \
+                    or tp.numel() != n_frames * self.C:
+                raise ValueError(f"meter_update: float32 values for {n_frames} x {self.C} channel-frames")
+            self._bind_stream(li)
+            out = torch.empty((n_frames * self.C, L.N_METERS), dtype=torch.float64, device=li.device)
+            self._check(L.lib().omega_meter_update(self._ctx, _ptr(li), _ptr(tp), int(n_frames), _ptr(out),
+                                                   L.MEM_DEVICE))
+            return out
         li = np.ascontiguousarray(lufs_inst, dtype=np.float32)
         tp = np.ascontiguousarray(tp_db, dtype=np.float32)
         out = np.empty((n_frames * self.C, L.N_METERS), np.float64)

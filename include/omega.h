@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define OMEGA_ABI_VERSION 1
+#define OMEGA_ABI_VERSION 2
 #define OMEGA_MAX_RES 4
 #define OMEGA_N_METERS 5 /* momentary, short_term, integrated, range, true_peak */
 
@@ -124,7 +124,17 @@ void omega_destroy(omega_ctx* ctx);
 const char* omega_last_error(const omega_ctx* ctx);
 const char* omega_version(void);
 /* Enqueue on a caller-owned hipStream_t (NULL = the null/default stream, e.g. PyTorch's default
- * stream). Contexts start on a private non-blocking stream. */
+ * stream). Contexts start on a private non-blocking stream. Switching streams orders the new stream
+ * (and the context's side stream) after the work already enqueued on the old one, once.
+ *
+ * Concurrency precondition of the default layout (omega_set_graphs): the batch kernel on this stream
+ * and the meter prep on the context's side stream wait for each other through device counters, so the
+ * two must be able to run at once. Each context owns two streams (its private one and the side stream;
+ * a graph-capture stream only once graphs are enabled); HIP maps streams onto GPU_MAX_HW_QUEUES
+ * hardware queues per process. Should the two share a queue, or another tenant hold every CU, the
+ * wait is bounded (OMEGA_POLL_LIMIT polls): that call's meter aggregates may be stale and OMEGA_EHIP
+ * is returned -- by the call itself for host memory, by the next call or omega_synchronize for
+ * device memory. Layouts other than 0 order the side stream by events and carry no such condition. */
 int omega_set_stream(omega_ctx* ctx, void* hip_stream);
 /* flags: bit 0 = HIP graphs: device-memory omega_process_frames calls are captured once per distinct
  * argument set and replayed afterwards (default off: measured slower than direct launches on MI355X,

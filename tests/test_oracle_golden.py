@@ -394,3 +394,17 @@ def test_capture_gate(golden):
     gated = (g["out"].reshape(-1, 512) == 0).all(axis=1) & (x.reshape(-1, 512) != 0).any(axis=1)
     assert gated.sum() >= 15  # chunks the gate zeroed (besides the exact-zero stretch)
     np.testing.assert_array_equal(R.capture_stream(x, gain=4.0), g["out"] * np.float32(4.0))
+
+
+def test_spectra_batch_matches_per_frame_chain():
+    """The whole-batch cfg3 oracle (omega_ref.spectra_batch, used by the GPU full-batch test) equals
+    the per-frame chain batched_fft -> map_to_bands / ChromaState().compute frame by frame."""
+    x = S.cfg3_batch(24)
+    st, en, comp = R.pipeline_band_table(FS, 512, 8192)
+    mag, bands, chroma = R.spectra_batch(x, st, en, comp, 512)
+    freqs = np.fft.rfftfreq(8192, 1 / FS)
+    for f in range(len(x)):
+        m = R.batched_fft(x[f], 8192, "hann")["magnitude"].astype(np.float32)
+        np.testing.assert_array_equal(mag[f], m)
+        np.testing.assert_array_equal(bands[f], R.map_to_bands(m, st, en, comp, 512))
+        np.testing.assert_allclose(chroma[f], R.ChromaState().compute(m, freqs), rtol=1e-12, atol=1e-15)
