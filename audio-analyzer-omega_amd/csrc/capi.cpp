@@ -67,6 +67,15 @@ constexpr int kBatchWaves = 8;  // waves of a batch_kernel workgroup (rfkern.hip
 // finish. (Round 1: one meter workgroup per 8 outputs of a 4096-frame batch took every slot and waited
 // until the poll bound expired.)
 constexpr int kMeterWgs = 64;
+// batch grid order (BatchPlan::pat, ::multi_start; A/B builds set them with -D)
+#ifndef OMEGA_PLAN_PAT
+#define OMEGA_PLAN_PAT 1
+#endif
+#ifndef OMEGA_PLAN_MULTI_AT
+#define OMEGA_PLAN_MULTI_AT 0
+#endif
+constexpr int kPlanPat = OMEGA_PLAN_PAT;
+constexpr int kPlanMultiAt = OMEGA_PLAN_MULTI_AT;
 
 struct DevBuf {
   void* p = nullptr;
@@ -925,11 +934,28 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   // the per-context scratch and keep the query kernels
   const bool in_grid = meters && do_tp && do_kw && n_frames > 0 && n_frames <= kChunkFrames;
   const int64_t n_mq = in_grid ? std::min<int64_t>((n + kBatchWaves - 1) / kBatchWaves, kMeterWgs) : 0;
+  // grid order: segment 0 | segment 1 | small resolutions, or with kPlanMultiAt = 1 segment 0 | small
+  // resolutions | segment 1
+  bp.pat = kPlanPat;
+  bp.multi_n = (int)nwg;
+  bp.seg_start[0] = 0;
+  int64_t body_end;
+  if (kPlanMultiAt == 1) {
+    // (segment 1 starts on a multiple of 8, so a frame's roles keep one XCD; the few blocks between
+    // return at once)
+    bp.multi_start = bp.seg_begin[1];
+    bp.seg_start[1] = (int)((bp.seg_begin[1] + nwg + 7) / 8 * 8);
+    body_end = bp.seg_start[1] + (int64_t)(bp.seg_begin[2] - bp.seg_begin[1]);
+  } else {
+    bp.seg_start[1] = bp.seg_begin[1];
+    bp.multi_start = bp.seg_begin[2];
+    body_end = end + nwg;
+  }
   // the grid's last segment (measured: placed before the small resolutions it holds 64 slots from
   // ~50 us on and the step is no shorter, 77.4-79.2 vs 77.0-78.0 us)
-  bp.q_begin = (int)(end + nwg);
+  bp.q_begin = (int)body_end;
   bp.q_n = (int)n_mq;
-  const int64_t grid = end + nwg + n_mq;
+  const int64_t grid = body_end + n_mq;
   if (grid > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
   MeterPrepParams mq{};
   std::vector<MeterPrepParams> mc;

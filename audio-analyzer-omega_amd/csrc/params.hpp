@@ -215,6 +215,11 @@ struct MultiPlan {
 //       used, tools/wgtrace.py. Role chunks of one workgroup per CU fill 90 % of it, but the shader
 //       clock drops from ~2120 to ~1890 MHz and the launch takes longer: the batch runs at the chip's
 //       power limit, so idle slots are not free time. DESIGN.md §8.)
+//   pat: the group order of a two-role segment: 0 alternating groups (each shader engine runs one
+//       role), 1 the period-8 order A B A B B A B A (seen by one XCD through blockIdx % 8, its engines
+//       get the roles in turn, so an engine's short workgroups do not wait behind another's long ones).
+//   seg_start / multi_start: where segment s and the small resolutions begin in the grid (the small
+//       resolutions after segment 1, or between the segments).
 struct BatchPlan {
   int seg_begin[3];
   int n_roles[2];
@@ -222,6 +227,9 @@ struct BatchPlan {
   int mr_res;
   MultiPlan multi;
   int q_begin, q_n;
+  int pat;
+  int seg_start[2];
+  int multi_start, multi_n;
 };
 
 // Fused spectrum analysis (cfg3): windowed rfft magnitude (A13) -> log-band max (A10) and raw

@@ -16,6 +16,12 @@
 // LDS slots are XOR-swizzled so every exchange is free of bank conflicts (ds_write_b64 groups of
 // 16 lanes, ds_read_b64 groups of 32); the natural-order slot map a3 (for consumers that read the
 // spectrum by frequency: untangles, magnitudes) costs at most one extra cycle on mirror reads.
+//
+// Exchange 2 needs no workgroup barrier: the rows k1 of exchange 1 and of exchange 2 share one
+// stride (P1 == P2R), and a wave's pass-2 threads (k1 = t / L: 2 rows for K = 8192, 4 for 4096) read
+// exactly the rows its exchange-2 writes and pass-3 reads touch -- no other wave reads or writes them
+// between exchange 1's barrier and the next transform's (or the caller's) barrier. Within the wave,
+// LDS operations complete in issue order; an lgkmcnt drain before the pass-3 reads makes that explicit.
 #pragma once
 #include "fft.hpp"
 
@@ -34,6 +40,12 @@ __device__ constexpr float kSin128[16] = {
     4.713967368e-01f, 5.141027442e-01f, 5.555702330e-01f, 5.956993045e-01f, 6.343932842e-01f,
     6.715589548e-01f};
 
+// This wave's LDS stores are complete before its next LDS reads (a wave-local exchange: no s_barrier)
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // lane l reads lane l ^ 1 (DPP quad_perm [1,0,3,2])
 __device__ __forceinline__ float lane_xor1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
@@ -46,12 +58,13 @@ struct RegFFT {
   static constexpr int L = K / 256;
   // LDS layouts (float2 slots), padded so that every slot is a per-thread base plus a compile-time
   // offset per register (ds_read/ds_write immediate offsets: no per-element address arithmetic):
-  //   exchange 1, element (t, k1):       P1 k1 + t
+  //   exchange 1, element (t, k1):       P1 k1 + t   (P1 = P2R: one row per k1 for both exchanges)
   //   exchange 2, element (u, k2, k1):   P2R k1 + P2C k2 + u
   //   spectrum, frequency n:             a3(n) = n + n/16 (+ 8 for n >= 4096 when K = 8192)
-  static constexpr int P1 = L == 32 ? 512 : 272;
+  static constexpr int P1 = L == 32 ? 544 : 272;
   static constexpr int P2R = L == 32 ? 544 : 272;
   static constexpr int P2C = L == 32 ? 34 : 17;
+  static_assert(P1 == P2R && 16 * P2R <= (K == 8192 ? 8712 : 4352), "exchange rows shared by both exchanges");
   static constexpr int kSlots = K == 8192 ? 8712 : 4352;  // LDS buffer size in float2
   // pass-2 twiddle table in LDS: t2[(k2 - 1) L + u] = W_K^{16 u k2}, k2 = 1..15, u < L (3.75 KiB for
   // K = 8192): 15 broadcast-free ds_read_b64 per pass instead of the 14-multiplication power chain
@@ -145,11 +158,11 @@ struct RegFFT {
         twiddle_t2(v, t2 + u);
       else
         twiddle(v, w2);
-      __syncthreads();  // every exchange-1 read is done
+      // (no barrier: the rows k1 are this wave's alone -- see the header)
       float2* bw = buf + P2R * k1 + u;
       static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
     }
-    __syncthreads();
+    wave_lds_sync();
     // pass 3
     if constexpr (L == 16) {
       const int k2 = t & 15, k1 = t >> 4;
@@ -199,11 +212,10 @@ struct RegFFT {
         twiddle_t2(v, t2 + u);
       else
         twiddle(v, w2);
-      __syncthreads();
-      float2* bw = buf + P2R * k1 + u;
+      float2* bw = buf + P2R * k1 + u;  // (this wave's rows: no barrier)
       static_for<0, 16>([&](auto k2) { bw[P2C * k2] = v[k2]; });
     }
-    __syncthreads();
+    wave_lds_sync();
     const int q = t & 1, k2 = (t >> 1) & 15, k1 = t >> 5;
     {
       const float2* b = buf + P2R * k1 + P2C * k2 + q;
@@ -220,7 +232,7 @@ struct RegFFT {
     const float2 send = q ? f0 : f15;
     const float2 recv = make_float2(lane_xor1(send.x), lane_xor1(send.y));
     const float2 out = q ? csub(recv, g) : cadd(f0, recv);
-    __syncthreads();  // every exchange-2 read is done
+    __syncthreads();  // every exchange-2 read is done (the natural-order slots span every wave's rows)
     buf[s3o(t) + (q ? o3o(15) : 0)] = out;
     __syncthreads();
   }

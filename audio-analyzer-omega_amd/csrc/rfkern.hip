@@ -691,11 +691,24 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
     OMEGA_WG_END(4);
     return;
   }
-  if (b < bp.seg_begin[2]) {
-    const int sg = b < bp.seg_begin[1] ? 0 : 1;
-    const int j = b - bp.seg_begin[sg], nr = bp.n_roles[sg];
-    const int role = bp.roles[sg][(j >> 3) % nr];
-    const int64_t cf = (int64_t)(j / (8 * nr)) * 8 + (j & 7);
+  const int len0 = bp.seg_begin[1], len1 = bp.seg_begin[2] - bp.seg_begin[1];
+  const int sg = (b >= bp.seg_start[0] && b < bp.seg_start[0] + len0) ? 0
+                 : (b >= bp.seg_start[1] && b < bp.seg_start[1] + len1) ? 1 : -1;
+  if (sg >= 0) {
+    const int j = b - bp.seg_start[sg], nr = bp.n_roles[sg];
+    int role;
+    int64_t cf;
+    if (nr == 2 && bp.pat == 1) {
+      // period-8 group order A B A B B A B A (0x5A: the B positions); a group's index among its role's
+      // groups = 4 per period + the same-role positions before it
+      const int g = j >> 3, per = g & 7, rb = (0x5A >> per) & 1;
+      role = bp.roles[sg][rb];
+      const int idx = 4 * (g >> 3) + __popc((rb ? 0x5A : 0xA5) & ((1 << per) - 1));
+      cf = (int64_t)idx * 8 + (j & 7);
+    } else {
+      role = bp.roles[sg][(j >> 3) % nr];
+      cf = (int64_t)(j / (8 * nr)) * 8 + (j & 7);
+    }
     if (cf >= sp.n_cf) return;
     if (role == 0) {
       batch_kw_role(kp, cf, tid, smem);
@@ -708,7 +721,8 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
     return;
   }
   const MultiPlan& mp = bp.multi;
-  const int w = b - bp.seg_begin[2];
+  const int w = b - bp.multi_start;
+  if (w < 0 || w >= bp.multi_n) return;
   int s = 0;
   while (s + 1 < mp.n_seg && w >= mp.wg_begin[s + 1]) ++s;
   const int r = mp.res[s];

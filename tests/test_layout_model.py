@@ -33,3 +33,10 @@ def test_tight_layout():
     pl = M.TightPlan4096()
     _check(pl, 4096)
     M.check_tight()
+
+
+def test_exchange2_is_wave_local():
+    """regfft.hpp drops the workgroup barriers around exchange 2: every slot a wave writes or reads
+    there lies in its own exchange-1 rows, which no other wave reads."""
+    for K in (8192, 4096):
+        assert M.wave_local_exchange2(K) == 0

@@ -44,7 +44,7 @@ class Plan:
     # ---- swizzles (float2 index -> LDS slot) ----
     # padded layouts: every slot is a per-thread base plus a compile-time offset per register
     def a1(self, t, k1):
-        return k1 * (512 if self.L == 32 else 272) + t
+        return k1 * (544 if self.L == 32 else 272) + t  # the same row stride as a2 (wave-local exchange 2)
 
     def a2(self, u, k2, k1):
         if self.L == 32:
@@ -222,3 +222,33 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def wave_local_exchange2(K):
+    """Exchange 2 is wave-local (regfft.hpp): the slots a wave's exchange-2 writes and pass-3 reads
+    touch lie in rows whose exchange-1 slots only that wave's pass-2 threads read. Returns the number
+    of violating slots (0)."""
+    P = Plan(K)
+    bad = 0
+    for w in range(P.NTH // 64):
+        own = set()
+        for tau in range(64 * w, 64 * w + 64):
+            u, k1 = P.p2(tau)
+            own |= {P.a1(u + P.L * r, k1) for r in range(16)}  # exchange-1 reads of this wave
+        rows = {a // P.a1(0, 1) for a in own}
+        touched = set()
+        for tau in range(64 * w, 64 * w + 64):
+            u, k1 = P.p2(tau)
+            touched |= {P.a2(u, k2, k1) for k2 in range(16)}
+            q, k2, k1b = P.p3(tau)
+            us = [q + 2 * i for i in range(16)] if P.L == 32 else list(range(16))
+            touched |= {P.a2(uu, k2, k1b) for uu in us}
+        bad += sum(1 for a in touched if a // P.a1(0, 1) not in rows)
+        # and no other wave reads those rows in exchange 1
+        for w2 in range(P.NTH // 64):
+            if w2 == w:
+                continue
+            for tau in range(64 * w2, 64 * w2 + 64):
+                u, k1 = P.p2(tau)
+                bad += sum(1 for r in range(16) if P.a1(u + P.L * r, k1) in touched)
+    return bad
