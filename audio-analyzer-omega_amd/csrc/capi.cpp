@@ -241,8 +241,6 @@ struct omega_ctx {
   unsigned* h_err = nullptr;
   unsigned* d_err = nullptr;
   int poll_limit = 1 << 22;
-  unsigned long long* d_prep_u = nullptr;  // meter_prep_kernel scratch: merged keys, staged sequence
-  float* d_prep_v = nullptr;
   float* d_lufs_scr = nullptr;  // omega_calculate_lufs: instantaneous values kept on the device
   int64_t lufs_scr_cap = 0;
   bool res_independent = false;  // no combine target has several owners: resolution kernels commute
@@ -330,12 +328,14 @@ struct omega_ctx {
   unsigned long long* d_skeys[2] = {};  // sorted gated history keys (double-buffered state)
   int* d_ns[2] = {};
   uint32_t* d_t0[2] = {};
-  float* d_core = nullptr;  // per-batch meter scratch
-  MeterExt* d_ext = nullptr;
-  int* d_ncore = nullptr;
-  int* d_next = nullptr;
-  int* d_gcount = nullptr;
-  double* d_gsum = nullptr;
+  // per-batch meter scratch, two sets by the state's parity (cur): the next batch's prep writes the
+  // other set from before its K-weighting values are in, while this batch's queries read this one
+  float* d_core[2] = {nullptr, nullptr};
+  MeterExt* d_ext[2] = {nullptr, nullptr};
+  int* d_ncore[2] = {nullptr, nullptr};
+  int* d_next[2] = {nullptr, nullptr};
+  int* d_gcount[2] = {nullptr, nullptr};
+  double* d_gsum[2] = {nullptr, nullptr};
   int HL = 0, HT = 0;
   // staging for OMEGA_MEM_HOST
   std::vector<DevBuf> stage;
@@ -686,14 +686,14 @@ int build_meter_state(omega_ctx* c) {
     if (!e) e = dalloc(c, &c->d_ns[b], C);
     if (!e) e = dalloc(c, &c->d_t0[b], C);
   }
-  if (!e) e = dalloc(c, &c->d_core, (size_t)C * kMeterSeqCap);
-  if (!e) e = dalloc(c, &c->d_ext, (size_t)C * kMeterSeqCap);
-  if (!e) e = dalloc(c, &c->d_ncore, C);
-  if (!e) e = dalloc(c, &c->d_next, C);
-  if (!e) e = dalloc(c, &c->d_gcount, (size_t)C * (kMeterSeqCap + 1));
-  if (!e) e = dalloc(c, &c->d_gsum, (size_t)C * (kMeterSeqCap + 1));
-  if (!e) e = dalloc(c, &c->d_prep_u, (size_t)C * kMeterSeqCap);
-  if (!e) e = dalloc(c, &c->d_prep_v, (size_t)C * kMeterSeqCap);
+  for (int b = 0; b < 2; ++b) {
+    if (!e) e = dalloc(c, &c->d_core[b], (size_t)C * kMeterSeqCap);
+    if (!e) e = dalloc(c, &c->d_ext[b], (size_t)C * kMeterSeqCap);
+    if (!e) e = dalloc(c, &c->d_ncore[b], C);
+    if (!e) e = dalloc(c, &c->d_next[b], C);
+    if (!e) e = dalloc(c, &c->d_gcount[b], (size_t)C * (kMeterSeqCap + 1));
+    if (!e) e = dalloc(c, &c->d_gsum[b], (size_t)C * (kMeterSeqCap + 1));
+  }
   if (!e) e = dalloc(c, &c->d_kw_done, 8);
   if (e) return e;
   if (!c->h_err) {
@@ -824,16 +824,14 @@ std::vector<MeterPrepParams> meter_chunks(omega_ctx* c, const float* lufs, const
     p.poll_limit = c->poll_limit;
     p.err_word = c->d_err;
     p.gate = (float)c->cfg.gate_lufs;
-    p.core = c->d_core;
-    p.ext = c->d_ext;
-    p.n_core = c->d_ncore;
-    p.n_ext = c->d_next;
-    p.gcount = c->d_gcount;
-    p.gsum = c->d_gsum;
+    p.core = c->d_core[a];
+    p.ext = c->d_ext[a];
+    p.n_core = c->d_ncore[a];
+    p.n_ext = c->d_next[a];
+    p.gcount = c->d_gcount[a];
+    p.gsum = c->d_gsum[a];
     p.out = out + f0 * C * OMEGA_N_METERS;
     p.parts = 3;
-    p.u_scr = c->d_prep_u;
-    p.v_scr = c->d_prep_v;
     v.push_back(p);
     c->cur = b;
   }

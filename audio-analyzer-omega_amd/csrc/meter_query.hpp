@@ -106,7 +106,8 @@ __device__ __forceinline__ void meter_query_wave(const MeterPrepParams& p, int64
   if (ng > 0) {
     integ = (gsum[n] - gsum[n - wi]) / ng;
     const uint32_t lo = window_lo(T0, nh, f, p.int_len), hi = T0 + (uint32_t)f;
-    const uint32_t clo = window_lo(T0, nh, F - 1, p.int_len), chi = T0;
+    // the core: the history's gated values inside every window of the batch (meters.hip)
+    const uint32_t clo = window_lo(T0, nh, F - 1, p.int_len), chi = T0 - 1u;
     const bool has_core = (int32_t)(chi - clo) >= 0;
     int want[4];
     double gam[2];

@@ -12,12 +12,13 @@
 //
 // The windows of one batch's frames slide by one frame each, so they share a core: the frames
 // [lo_{F-1}, hi_0] that lie in every window. Per batch:
-//   meter_prep_kernel  (one 1024-thread workgroup per channel): sort the batch's gated keys, merge
-//     them with the sorted history by rank (merge-path positions: own index + binary-search rank in the
-//     other list), split the merged list into the sorted CORE values and the sorted EXTRA values
-//     (gated values outside the core, at most 2(F-1)), each extra tagged with its frame index and the
-//     number of core values below it; write the next sorted history (dropping keys older than the
-//     window) the same way; prefix-count/sum the gated values in time order; roll the histories.
+//   meter_prep_kernel  (one 1024-thread workgroup per channel): the sorted CORE values (the history's
+//     gated values inside every window of the batch) and the sorted EXTRA values (the other gated
+//     values of the batch's windows: the evicted history ones and the batch's own, at most 2F), each
+//     extra tagged with its frame index and the number of core values below it -- merge-path
+//     positions from binary-search ranks; the gated count / sum prefixes in time order; the next
+//     sorted history (dropping keys older than the window) the same way; the history rolled. The
+//     history's part runs before the batch's K-weighting values are in (see the kernel).
 //   meter_query_kernel (one wave per frame): gated count and sum from the time-order prefixes. The
 //     frame's gated window is core + the extras inside its window; extra j (in value order among
 //     those) sits at merged rank j + its core count, so the k-th order statistic is either such an
@@ -158,294 +159,324 @@ __device__ __forceinline__ void st_wt(MeterExt* q, const MeterExt& e) {
                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The stream's LUFS_inst sequence over [T0 - nh, T0 + F) lives in LDS (V); every global input is
-// fetched once, up front.
+// Two phases around the wait for the batch's K-weighting count, so that everything the history alone
+// determines is done while the batch runs, and only the batch's own values remain after the count:
+//   before: stage the sorted history keys A; the CORE = the history's gated values in every window of
+//     the batch (absolute index >= clo = the last frame's window start), sorted -- a compaction of A by
+//     an exclusive in-core prefix cpA; the history part of the time-order gated count / sum prefixes;
+//     the kept prefix over A for the next sorted history; the history part of the next LUFS history.
+//   after:  the batch's gated keys, rank-sorted (B); the EXTRAS = the evicted history keys (A minus the
+//     core) merged with B by rank, each with its core count below (cpA at its rank in A); the batch
+//     part of the time-order prefixes; publish (write-through) and count in -- then, off the critical
+//     path, the next sorted history (kept A merged with kept B) and the rest of the state.
+// The core holds history frames only (batch frame 0, in every window too, is an extra): the queries
+// take chi = T0 - 1.
 __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
-  __shared__ unsigned long long B[kNewCap];   // the batch's gated keys, sorted
-  __shared__ unsigned long long A[kHistCap];  // the history's gated keys, sorted
-  // A merged with B, and the time-ordered LUFS_inst (history ++ batch), in per-channel global scratch
-  // (L2-resident): the kernel's 72 KiB of LDS then fit beside one batch workgroup (71.9 KiB) on a CU,
-  // so the prep -- resident from before the batch starts -- takes one batch slot instead of a whole
-  // CU (with 144 KiB it kept its XCD at 56 of 64 slots: tools/wgtrace.py --meters)
-  unsigned long long* U = p.u_scr + (int64_t)blockIdx.x * kSeqCap;
-  float* V = p.v_scr + (int64_t)blockIdx.x * kSeqCap;
-  __shared__ int kp[kHistCap];                // exclusive prefix of kept flags over A (key order)
-  // exclusive prefix of kept flags over B (key order); before that (rank sort) the batch's 64-bit
-  // keys in time order (~0ull: not gated)
-  // (+2: the rank sort's 64-bit keys K64[0..F] overlay it, F <= 1024 -- K64[F] pads the last 16-byte read)
-  __shared__ __attribute__((aligned(16))) int kb[kNewCap + 2];
+  __shared__ unsigned long long A[kHistCap];  // the history's gated keys, sorted (32 KiB)
+  __shared__ unsigned long long B[kNewCap];   // the batch's gated keys, sorted (16 KiB)
+  __shared__ unsigned short cpA[kHistCap];  // exclusive in-core prefix over A (cpA[ns] = core size)
+  __shared__ unsigned short kpA[kHistCap];  // exclusive kept prefix over A (next sorted history)
+  // the rank sort's time-ordered batch keys (F <= 1024; K64[F] pads the last 16-byte read); after the
+  // sort, the exclusive kept prefix over B
+  __shared__ __attribute__((aligned(16))) unsigned long long K64[1024 + 2];
+  unsigned short* kbB = reinterpret_cast<unsigned short*>(K64);
   __shared__ int wsa[16], wsb[16], wsc[16];
   __shared__ double wsd[16];
-  unsigned long long* K64 = reinterpret_cast<unsigned long long*>(kb);
   const int c = blockIdx.x, tid = threadIdx.x;
   OMEGA_MARK(c, 0);
-  if (p.wait_ctr) {
-    // the batch's LUFS_inst values come from batch_kernel on another stream: one lane polls the count
-    // (relaxed, bounded), then ONE agent-scope acquire before any wave reads them
-    if (tid == 0) {
-      bool met = false;
-      for (int i = 0; i < p.poll_limit; ++i) {
-        if ((int)(__hip_atomic_load(p.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - p.wait_target) >= 0) {
-          met = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(4);
-      }
-      if (!met && p.err_word)
-        __hip_atomic_store(p.err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-  }
-  OMEGA_MARK(c, 1);
   const int C = p.C, F = (int)p.n_frames;
   const uint32_t T0 = p.t0_in[c];
   const int nh = p.n_l_in[c], ns = p.n_s_in[c];
   const int L = nh + F;
   const int64_t thr = (int64_t)T0 + F - p.HL;  // oldest absolute index the next batch's windows reach
+  const uint32_t clo = window_lo(T0, nh, F - 1, p.int_len), chi = T0 - 1u;
+  const bool has_core = (int32_t)(chi - clo) >= 0;
   const float gate = p.gate;
+  float* core = p.core + (int64_t)c * kSeqCap;
+  MeterExt* ext = p.ext + (int64_t)c * kSeqCap;
+  int* gp = p.gcount + (int64_t)c * (kSeqCap + 1);
+  double* gsum = p.gsum + (int64_t)c * (kSeqCap + 1);
   OMEGA_STAMP(0);
-  // 1) stage the sequence and the sorted history (loads of a thread issued together); the batch's
-  // value keys for the rank sort
+  // ---- before the count ----
+  constexpr int PA = kHistCap / 1024;
+  const int ph = (nh + 1023) / 1024, h0 = tid * ph;  // this thread's run of the history sequence
+  float hv[(kHistCap + 1023) / 1024];
 #pragma unroll
-  for (int q = 0; q < kSeqCap / 1024; ++q) {
-    const int u = q * 1024 + tid;
-    if (u < L) {
-      const float v = u < nh ? p.hist_l_in[(int64_t)c * p.HL + u] : p.lufs[(int64_t)(u - nh) * C + c];
-      V[u] = v;
-      if (u >= nh && F <= 1024)
-        K64[u - nh] = v > gate ? ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)(u - nh))
-                               : ~0ull;
-    }
-  }
-  if (F <= 1024 && tid == 0) K64[F] = ~0ull;  // padding of the last 16-byte read
-#pragma unroll
-  for (int q = 0; q < kHistCap / 1024; ++q) {
-    const int i = q * 1024 + tid;
+  for (int q = 0; q < PA; ++q) {
+    const int i = tid * PA + q;
     if (i < ns) A[i] = p.skeys_in[(int64_t)c * p.HL + i];
   }
+#pragma unroll
+  for (int q = 0; q < (kHistCap + 1023) / 1024; ++q)
+    hv[q] = q < ph && h0 + q < nh ? p.hist_l_in[(int64_t)c * p.HL + h0 + q] : -INFINITY;
   __syncthreads();
-  OMEGA_STAMP(1);
-  // 2) sort the batch's gated keys (distinct: they carry the frame index). Up to 1024 frames: rank
-  // sort, P threads per key (adjacent lanes) each counting the smaller keys of a 1/P slice (16-byte
-  // reads); beyond: bitonic.
-  int Gn;
-  int Fp = 1;
-  while (Fp < F) Fp <<= 1;
-  if (Fp <= 1024) {
-    const int P = min(64, 1024 / Fp);
-    const int f = tid / P, part = tid % P;
-    const int len = (((F + P - 1) / P) + 1) & ~1, g0 = part * len, g1 = min(F, g0 + len);
-    const unsigned long long kf = f < F ? K64[f] : ~0ull;
-    int rank = 0;
-    if (kf != ~0ull) {
-#pragma unroll 8
-      for (int g = g0; g < g1; g += 2) {
-        const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(K64 + g);
-        rank += q.x < kf;
-        rank += q.y < kf;
-      }
-    }
-    for (int o = 1; o < P; o <<= 1) rank += __shfl_xor(rank, o, 64);
-    Gn = __syncthreads_count(part == 0 && kf != ~0ull);
-    if (part == 0 && kf != ~0ull) B[rank] = kf;
-  } else {
-    auto bkey = [&](int f) -> unsigned long long {
-      const float v = V[nh + f];
-      return v > gate ? ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)f) : ~0ull;
-    };
-    for (int f = tid; f < Fp; f += 1024) B[f] = f < F ? bkey(f) : ~0ull;
-    __syncthreads();
-    for (int k = 2; k <= Fp; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < Fp; i += 1024) {
-          const int l = i ^ j;
-          if (l > i) {
-            const unsigned long long a = B[i], b = B[l];
-            if ((a > b) == ((i & k) == 0)) {
-              B[i] = b;
-              B[l] = a;
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-    int gn_part = 0;
-    for (int i = tid; i < Fp; i += 1024) gn_part += B[i] != ~0ull;
-    Scan4 tot;
-    block_excl_scan4(Scan4{gn_part, 0, 0, 0.0}, wsa, wsb, wsc, wsd, tid, tot);
-    Gn = tot.a;
-  }
-  __syncthreads();  // B complete; K64 (kb) free for the kept prefixes
-  OMEGA_STAMP(2);
-  // 3) kept flags (absolute index >= thr) and their key-order prefixes, for A and B
-  constexpr int PA = kHistCap / 1024, PB = kNewCap / 1024;
-  int Ka, Kb;
+  int inc[PA], kep[PA];
   {
-    int fa[PA], fb[PB], sa = 0, sb = 0;
+    int sc = 0, sk = 0, gi = 0;
+    double gd = 0.0;
 #pragma unroll
     for (int q = 0; q < PA; ++q) {
       const int i = tid * PA + q;
-      fa[q] = i < ns && (int64_t)(uint32_t)A[i] >= thr;
-      sa += fa[q];
+      const uint32_t t = (uint32_t)A[i];
+      inc[q] = i < ns && has_core && (uint32_t)(t - clo) <= chi - clo;
+      kep[q] = i < ns && (int64_t)t >= thr;
+      sc += inc[q];
+      sk += kep[q];
     }
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      const int i = tid * PB + q;
-      fb[q] = i < Gn && (int64_t)(uint32_t)B[i] >= thr;
-      sb += fb[q];
-    }
+    for (int q = 0; q < (kHistCap + 1023) / 1024; ++q)
+      if (hv[q] > gate) {
+        ++gi;
+        gd += (double)hv[q];
+      }
     Scan4 tot;
-    const Scan4 e = block_excl_scan4(Scan4{sa, sb, 0, 0.0}, wsa, wsb, wsc, wsd, tid, tot);
-    int ea = e.a, eb = e.b;
+    const Scan4 e = block_excl_scan4(Scan4{sc, sk, gi, gd}, wsa, wsb, wsc, wsd, tid, tot);
+    int ec = e.a, ek = e.b, eg = e.c;
+    double ed = e.d;
 #pragma unroll
     for (int q = 0; q < PA; ++q) {
-      kp[tid * PA + q] = ea;
-      ea += fa[q];
+      const int i = tid * PA + q;
+      cpA[i] = (unsigned short)ec;
+      kpA[i] = (unsigned short)ek;
+      if (inc[q]) st_wt(core + ec, unkey((uint32_t)(A[i] >> 32)));
+      ec += inc[q];
+      ek += kep[q];
     }
+    if (tid == 0) st_wt(p.n_core + c, tot.a);
+    // the history part of the time-order prefixes (exclusive at each index)
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      kb[tid * PB + q] = eb;
-      eb += fb[q];
-    }
-    Ka = tot.a;
-    Kb = tot.b;
-  }
-  __syncthreads();
-  OMEGA_STAMP(3);
-  // 4) the merged list U, and the next sorted history (kept ones), by rank
-  unsigned long long* S = p.skeys_out + (int64_t)c * p.HL;
-  {
-    unsigned long long av[PA];
-    int ra[PA];
-#pragma unroll
-    for (int q = 0; q < PA; ++q) av[q] = q * 1024 + tid < ns ? A[q * 1024 + tid] : ~0ull;
-    lower_ranks<PA>(B, Gn, av, ra);
-#pragma unroll
-    for (int q = 0; q < PA; ++q) {
-      const int i = q * 1024 + tid, r = ra[q];
-      if (i < ns) {
-        U[i + r] = av[q];
-        if ((int64_t)(uint32_t)av[q] >= thr) S[kp[i] + (r < Gn ? kb[r] : Kb)] = av[q];
+    for (int q = 0; q < (kHistCap + 1023) / 1024; ++q) {
+      const int u = h0 + q;
+      if (q < ph && u < nh) {
+        st_wt(gp + u, eg);
+        st_wt(gsum + u, ed);
+        if (hv[q] > gate) {
+          ++eg;
+          ed += (double)hv[q];
+        }
       }
     }
-  }
-  {
-    unsigned long long bv[PB];
-    int rb[PB];
-#pragma unroll
-    for (int q = 0; q < PB; ++q) bv[q] = q * 1024 + tid < Gn ? B[q * 1024 + tid] : ~0ull;
-    lower_ranks<PB>(A, ns, bv, rb);
-#pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      const int j = q * 1024 + tid, r = rb[q];
-      if (j < Gn) {
-        U[j + r] = bv[q];
-        if ((int64_t)(uint32_t)bv[q] >= thr) S[kb[j] + (r < ns ? kp[r] : Ka)] = bv[q];
+    // the history's gated totals (the batch part continues from them)
+    const int hist_gi = tot.c;
+    const double hist_gd = tot.d;
+    // the next LUFS history: its part that comes from this history
+    const int klen = min(p.HL, L);
+    for (int i = tid; i < klen; i += 1024) {
+      const int src = L - klen + i;
+      if (src < nh) p.hist_l_out[(int64_t)c * p.HL + i] = p.hist_l_in[(int64_t)c * p.HL + src];
+    }
+    // (every index of cpA / kpA below kHistCap is written: the ones at ns and past it hold the totals)
+    OMEGA_STAMP(1);
+    // ---- the batch's K-weighting values ----
+    if (p.wait_ctr) {
+      // they come from batch_kernel on another stream: one lane polls the count (relaxed, bounded),
+      // then ONE agent-scope acquire before any wave reads them
+      if (tid == 0) {
+        bool met = false;
+        for (int i = 0; i < p.poll_limit; ++i) {
+          if ((int)(__hip_atomic_load(p.wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - p.wait_target) >= 0) {
+            met = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(4);
+        }
+        if (!met && p.err_word)
+          __hip_atomic_store(p.err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-  }
-  __syncthreads();
-  OMEGA_STAMP(4);
-  // 5) split U into core / extra (a contiguous run per thread), and the gated count / sum prefixes
-  // in time order over [T0 - nh, T0 + F) (a contiguous run of V per thread)
-  const int G = ns + Gn;
-  const uint32_t clo = window_lo(T0, nh, F - 1, p.int_len), chi = T0;
-  const bool has_core = (int32_t)(chi - clo) >= 0;
-  auto in_core = [&](unsigned long long k) { return has_core && (uint32_t)((uint32_t)k - clo) <= chi - clo; };
-  const int pu = (G + 1023) / 1024, u0 = tid * pu;
-  const int pv = (L + 1023) / 1024, v0 = tid * pv;
-  int cc = 0, ce = 0, gi = 0;
-  double gd = 0.0;
-  for (int q = 0; q < pu; ++q) {
-    const int u = u0 + q;
-    if (u < G) {
-      const bool core = in_core(U[u]);
-      cc += core;
-      ce += !core;
-    }
-  }
-  for (int q = 0; q < pv; ++q) {
-    const int u = v0 + q;
-    if (u < L && V[u] > gate) {
-      ++gi;
-      gd += (double)V[u];
-    }
-  }
-  Scan4 tot;
-  const Scan4 ex = block_excl_scan4(Scan4{cc, ce, gi, gd}, wsa, wsb, wsc, wsd, tid, tot);
-  int ec = ex.a, ee = ex.b, eg = ex.c;
-  double ed = ex.d;
-  OMEGA_STAMP(5);
-  float* core = p.core + (int64_t)c * kSeqCap;
-  MeterExt* ext = p.ext + (int64_t)c * kSeqCap;
-  for (int q = 0; q < pu; ++q) {
-    const int u = u0 + q;
-    if (u < G) {
-      const unsigned long long k = U[u];
-      if (in_core(k)) {
-        st_wt(core + ec++, unkey((uint32_t)(k >> 32)));
-      } else {
-        st_wt(ext + ee++, MeterExt{unkey((uint32_t)(k >> 32)), (uint32_t)k, ec, 0});
-      }
-    }
-  }
-  int* gp = p.gcount + (int64_t)c * (kSeqCap + 1);
-  double* gsum = p.gsum + (int64_t)c * (kSeqCap + 1);
-  for (int q = 0; q < pv; ++q) {
-    const int u = v0 + q;
-    if (u < L) {
-      st_wt(gp + u, eg);
-      st_wt(gsum + u, ed);
-      if (V[u] > gate) {
-        ++eg;
-        ed += (double)V[u];
-      }
-    }
-  }
-  if (v0 < L && v0 + pv >= L) {  // the run that ends the sequence holds the totals
-    st_wt(gp + L, eg);
-    st_wt(gsum + L, ed);
-  }
-  if (u0 < G && u0 + pu >= G) {
-    st_wt(p.n_core + c, ec);
-    st_wt(p.n_ext + c, ee);
-  }
-  if (tid == 0) {
-    if (L == 0) {
-      st_wt(gp, 0);
-      st_wt(gsum, 0.0);
-    }
-    if (G == 0) {
-      st_wt(p.n_core + c, 0);
-      st_wt(p.n_ext + c, 0);
-    }
-    p.n_s_out[c] = Ka + Kb;
-    p.t0_out[c] = T0 + (uint32_t)F;
-  }
-  OMEGA_STAMP(6);
-  // 6) time-ordered LUFS history for the next batch (the TP history rolls in meter_query_kernel)
-  const int klen = min(p.HL, L);
-  for (int i = tid; i < klen; i += 1024) p.hist_l_out[(int64_t)c * p.HL + i] = V[L - klen + i];
-  if (tid == 0) p.n_l_out[c] = klen;
-  OMEGA_STAMP(7);
-  OMEGA_MARK(c, 2);
-  if (p.q_done) {
-    // count this channel's prep in for the batch's meter segment: every wave's (write-through) stores
-    // drained, then a relaxed add. INVARIANT: every field the in-grid queries (meter_query.hpp) read
-    // is stored above with st_wt (write-through, agent scope): core[], ext[], gp[] (time-order gated
-    // prefix counts), gsum[] (their sums), n_core[c], n_ext[c]; the LUFS history, its count and the
-    // next frame index (hist_l_out, n_l_out, n_s_out, t0_out) are read only by the NEXT batch's prep and
-    // queries, which run behind the next prep, itself ordered behind this kernel on fork[0]. A plain store to one of the former would reach the
-    // query on another XCD late, without any warning: there is no release here for the query's poll to
-    // synchronise with -- the ordering rests on sc1 stores being acknowledged once coherent across
-    // XCDs, then this vmcnt drain.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(p.q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    OMEGA_MARK(c, 1);
+    OMEGA_STAMP(2);
+    // ---- after the count ----
+    // 1) the batch's values (thread f < F holds frame f; two per thread above 1024 frames) and its
+    // gated keys
+    const int pf = (F + 1023) / 1024;
+    float bv[kNewCap / 1024];
+#pragma unroll
+    for (int q = 0; q < kNewCap / 1024; ++q) {
+      const int f = tid * pf + q;
+      bv[q] = q < pf && f < F ? p.lufs[(int64_t)f * C + c] : -INFINITY;
+    }
+    auto bkey = [&](int f, float v) -> unsigned long long {
+      return v > gate ? ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)f) : ~0ull;
+    };
+    // 2) sort the batch's gated keys (distinct: they carry the frame index). Up to 1024 frames: rank
+    // sort, P threads per key (adjacent lanes) each counting the smaller keys of a 1/P slice (16-byte
+    // reads); beyond: bitonic.
+    int Gn;
+    int Fp = 1;
+    while (Fp < F) Fp <<= 1;
+    if (Fp <= 1024) {
+      if (tid < F) K64[tid] = bkey(tid, bv[0]);
+      if (tid == 0) K64[F] = ~0ull;
+      __syncthreads();
+      const int P = min(64, 1024 / Fp);
+      const int f = tid / P, part = tid % P;
+      const int len = (((F + P - 1) / P) + 1) & ~1, g0 = part * len, g1 = min(F, g0 + len);
+      const unsigned long long kf = f < F ? K64[f] : ~0ull;
+      int rank = 0;
+      if (kf != ~0ull) {
+#pragma unroll 8
+        for (int g = g0; g < g1; g += 2) {
+          const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(K64 + g);
+          rank += q.x < kf;
+          rank += q.y < kf;
+        }
+      }
+      for (int o = 1; o < P; o <<= 1) rank += __shfl_xor(rank, o, 64);
+      Gn = __syncthreads_count(part == 0 && kf != ~0ull);
+      if (part == 0 && kf != ~0ull) B[rank] = kf;
+    } else {
+      for (int i = tid; i < Fp; i += 1024) B[i] = ~0ull;
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < kNewCap / 1024; ++q) {
+        const int f = tid * pf + q;
+        if (q < pf && f < F) B[f] = bkey(f, bv[q]);
+      }
+      __syncthreads();
+      for (int k = 2; k <= Fp; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = tid; i < Fp; i += 1024) {
+            const int l = i ^ j;
+            if (l > i) {
+              const unsigned long long x = B[i], y = B[l];
+              if ((x > y) == ((i & k) == 0)) {
+                B[i] = y;
+                B[l] = x;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      int gn_part = 0;
+      for (int i = tid; i < Fp; i += 1024) gn_part += B[i] != ~0ull;
+      Scan4 t2;
+      block_excl_scan4(Scan4{gn_part, 0, 0, 0.0}, wsa, wsb, wsc, wsd, tid, t2);
+      Gn = t2.a;
+    }
+    __syncthreads();  // B complete; K64 free
+    OMEGA_STAMP(3);
+    // 3) the extras: B[j] at j + (evicted history keys below it), with rc = core keys below it; the
+    // evicted A[i] at (i - cpA[i]) + (batch keys below it), rc = cpA[i]. Beside them the batch part of
+    // the time-order prefixes and the kept flags over B.
+    constexpr int PB = kNewCap / 1024;
+    unsigned long long bk[PB];
+    int ra[PB];
+#pragma unroll
+    for (int q = 0; q < PB; ++q) bk[q] = tid * PB + q < Gn ? B[tid * PB + q] : ~0ull;
+    lower_ranks<PB>(A, ns, bk, ra);
+    unsigned long long ak[PA];
+    int rb[PA];
+#pragma unroll
+    for (int q = 0; q < PA; ++q) ak[q] = tid * PA + q < ns ? A[tid * PA + q] : ~0ull;
+    lower_ranks<PA>(B, Gn, ak, rb);
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int j = tid * PB + q;
+      if (j < Gn) {
+        const int cb = cpA[ra[q]];
+        st_wt(ext + j + (ra[q] - cb), MeterExt{unkey((uint32_t)(bk[q] >> 32)), (uint32_t)bk[q], cb, 0});
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PA; ++q) {
+      const int i = tid * PA + q;
+      if (i < ns && !inc[q]) {
+        const int ci = cpA[i];
+        st_wt(ext + (i - ci) + rb[q], MeterExt{unkey((uint32_t)(ak[q] >> 32)), (uint32_t)ak[q], ci, 0});
+      }
+    }
+    {
+      // batch part of the prefixes: frame f's exclusive prefix at index nh + f, the total at nh + F
+      int gi = 0, sk = 0;
+      double gd = 0.0;
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int f = tid * pf + q;
+        if (q < pf && f < F && bv[q] > gate) {
+          ++gi;
+          gd += (double)bv[q];
+        }
+        const int j = tid * PB + q;
+        sk += j < Gn && (int64_t)(uint32_t)bk[q] >= thr;
+      }
+      Scan4 t3;
+      const Scan4 e3 = block_excl_scan4(Scan4{gi, sk, 0, gd}, wsa, wsb, wsc, wsd, tid, t3);
+      int eg2 = hist_gi + e3.a;
+      double ed2 = hist_gd + e3.d;
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int f = tid * pf + q;
+        if (q < pf && f < F) {
+          st_wt(gp + nh + f, eg2);
+          st_wt(gsum + nh + f, ed2);
+          if (bv[q] > gate) {
+            ++eg2;
+            ed2 += (double)bv[q];
+          }
+        }
+      }
+      if (tid == 0) {
+        st_wt(gp + L, hist_gi + t3.a);
+        st_wt(gsum + L, hist_gd + t3.d);
+        st_wt(p.n_ext + c, (ns - (int)cpA[ns]) + Gn);
+      }
+      // (every index of kbB below kNewCap is written: the ones at Gn and past it hold the total)
+      int ek2 = e3.b;
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const int j = tid * PB + q;
+        kbB[j] = (unsigned short)ek2;
+        ek2 += j < Gn && (int64_t)(uint32_t)bk[q] >= thr;
+      }
+      if (tid == 0) kbB[kNewCap] = (unsigned short)t3.b;  // (Gn = kNewCap)
+    }
+    OMEGA_STAMP(4);
+    OMEGA_MARK(c, 2);
+    if (p.q_done) {
+      // count this channel's prep in for the batch's meter segment: every wave's (write-through) stores
+      // drained, then a relaxed add. INVARIANT: every field the in-grid queries (meter_query.hpp) read
+      // is stored above with st_wt (write-through, agent scope): core[], ext[], gp[] (time-order gated
+      // prefix counts), gsum[] (their sums), n_core[c], n_ext[c]; the next state (hist_l_out, n_l_out,
+      // skeys_out, n_s_out, t0_out, written below) is read only by the NEXT batch's prep and queries,
+      // which run behind the next prep, itself ordered behind this kernel on fork[0]. A plain store to
+      // one of the former would reach the query on another XCD late, without any warning: there is no
+      // release here for the query's poll to synchronise with -- the ordering rests on sc1 stores being
+      // acknowledged once coherent across XCDs, then this vmcnt drain.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(p.q_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __syncthreads();  // (kbB complete)
+    }
+    // ---- the next state (off the meter queries' path) ----
+    const int Ka = kpA[ns], Kb = kbB[Gn];
+    unsigned long long* S = p.skeys_out + (int64_t)c * p.HL;
+#pragma unroll
+    for (int q = 0; q < PA; ++q) {
+      const int i = tid * PA + q;
+      if (i < ns && kep[q]) S[kpA[i] + kbB[rb[q]]] = ak[q];
+    }
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int j = tid * PB + q;
+      if (j < Gn && (int64_t)(uint32_t)bk[q] >= thr) S[kbB[j] + kpA[ra[q]]] = bk[q];
+    }
+    for (int i = tid; i < klen; i += 1024) {
+      const int src = L - klen + i;
+      if (src >= nh) p.hist_l_out[(int64_t)c * p.HL + i] = p.lufs[(int64_t)(src - nh) * C + c];
+    }
+    if (tid == 0) {
+      p.n_s_out[c] = Ka + Kb;
+      p.t0_out[c] = T0 + (uint32_t)F;
+      p.n_l_out[c] = klen;
+    }
   }
+  OMEGA_STAMP(5);
 }
 
 // One wave per output (f, c); workgroup (0, c) also rolls the channel's true-peak history. parts

@@ -153,9 +153,6 @@ struct MeterPrepParams {
   // (OMEGA_EHIP instead of silently stale meters)
   int poll_limit;
   unsigned* err_word;
-  // meter_prep_kernel's global scratch ([C, kMeterSeqCap] each): the merged keys, the staged sequence
-  unsigned long long* u_scr;
-  float* v_scr;
 };
 
 struct BandParams {

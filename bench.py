@@ -565,7 +565,11 @@ def cpu_calibration():
 
 def cpu_baseline(seconds):
     """The oracle (numpy/scipy restatement of the reference path, one core) on the first frames of
-    the same workload until the time budget is spent."""
+    the same workload until the time budget is spent -- the reference's steady state: windows, weight
+    tables and filter coefficients are computed once (as MultiResolutionFFT._setup_windows and
+    ProfessionalMetering.__init__ do), the meter deques carried frame to frame. `calibration` holds the
+    restatement-vs-reference ratio measured in the build container (tools/cpu_calibrate.py: the
+    reference with one MultiResolutionFFT and reset_all_buffers() per frame)."""
     os.environ.setdefault("OMP_NUM_THREADS", "1")
     from oracle import omega_ref as R
     x = cfg2_input(64)
@@ -582,8 +586,8 @@ def cpu_baseline(seconds):
             break
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "channel-frames/s", "cores": 1, "kind": "port", "cpu_model": cpu_model(),
-            "sample": f"{n} channel-frames of cfg2 (oracle: MRFFT 16k/8k/4k/1k + combine(512) + K-LUFS + "
-                      f"4x TP + meter deques), {dt:.1f} s, OMP_NUM_THREADS=1",
+            "sample": f"{n} channel-frames of cfg2 (oracle, steady state: MRFFT 16k/8k/4k/1k + combine(512) + "
+                      f"K-LUFS + 4x TP + meter deques), {dt:.1f} s, OMP_NUM_THREADS=1",
             "calibration": cpu_calibration()}
 
 

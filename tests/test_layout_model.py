@@ -40,3 +40,25 @@ def test_exchange2_is_wave_local():
     there lies in its own exchange-1 rows, which no other wave reads."""
     for K in (8192, 4096):
         assert M.wave_local_exchange2(K) == 0
+
+
+def test_meter_prep_model_matches_oracle():
+    """The meter prep / query index algebra (tools/model/meter_model.py restates meters.hip's core /
+    extras split by rank, the time-order prefixes and the next sorted history) equals the oracle's
+    MeterState over random batches: gated and ungated values, ties, a silent stretch, batch sizes
+    across the 3600-frame window's eviction."""
+    import numpy as np
+    import meter_model as MM
+    from oracle import omega_ref as R
+    rng = np.random.default_rng(4)
+    n = 4300
+    li = rng.uniform(-85, -5, n).astype(np.float32)
+    li[500:900] = -95.0
+    li[1000:1100] = np.float32(-23.0)
+    tp = rng.uniform(-40, 0, n).astype(np.float32)
+    m = MM.Model()
+    cuts = [0, 1, 7, 300, 1324, 2400, 3900, 4299, n]
+    got = np.concatenate([m.batch(li[a:b], tp[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    st = R.MeterState(48000)
+    ref = np.array([list(st.update(np.ones(1), float(li[f]), float(tp[f])).values()) for f in range(n)])
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-9)
