@@ -67,15 +67,7 @@ constexpr int kBatchWaves = 8;  // waves of a batch_kernel workgroup (rfkern.hip
 // finish. (Round 1: one meter workgroup per 8 outputs of a 4096-frame batch took every slot and waited
 // until the poll bound expired.)
 constexpr int kMeterWgs = 64;
-// batch grid order (BatchPlan::pat, ::multi_start; A/B builds set them with -D)
-#ifndef OMEGA_PLAN_PAT
-#define OMEGA_PLAN_PAT 1
-#endif
-#ifndef OMEGA_PLAN_MULTI_AT
-#define OMEGA_PLAN_MULTI_AT 0
-#endif
-constexpr int kPlanPat = OMEGA_PLAN_PAT;
-constexpr int kPlanMultiAt = OMEGA_PLAN_MULTI_AT;
+
 
 struct DevBuf {
   void* p = nullptr;
@@ -902,6 +894,8 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   auto add = [&](int sg, int role, bool on) {
     if (on) seg[sg][ns[sg]++] = role;
   };
+  // (measured: the true peaks in segment 0 beside the K-weighting, the 16384-point resolution in
+  // segment 1, with or without the small resolutions before it: step 73.5-75.1 vs 68.8-70.5 us)
   add(0, 0, do_kw);        // segment 0: K-weighting and the 16384-point resolution, groups of 8 frames
   add(0, 2, mr >= 0);
   add(1, 1, do_tp);        // segment 1: the true peaks
@@ -932,23 +926,15 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   // the per-context scratch and keep the query kernels
   const bool in_grid = meters && do_tp && do_kw && n_frames > 0 && n_frames <= kChunkFrames;
   const int64_t n_mq = in_grid ? std::min<int64_t>((n + kBatchWaves - 1) / kBatchWaves, kMeterWgs) : 0;
-  // grid order: segment 0 | segment 1 | small resolutions, or with kPlanMultiAt = 1 segment 0 | small
-  // resolutions | segment 1
-  bp.pat = kPlanPat;
+  // grid order: segment 0 | segment 1 | small resolutions (measured: the small resolutions between the
+  // segments, step 80.4-81.3 vs 76.6-77.5 us, round 4); segment 0 in the period-8 role order
+  // (BatchPlan::pat: batch kernel 65.7-66.1 vs 70.9-71.5 us)
+  bp.pat = 1;
   bp.multi_n = (int)nwg;
   bp.seg_start[0] = 0;
-  int64_t body_end;
-  if (kPlanMultiAt == 1) {
-    // (segment 1 starts on a multiple of 8, so a frame's roles keep one XCD; the few blocks between
-    // return at once)
-    bp.multi_start = bp.seg_begin[1];
-    bp.seg_start[1] = (int)((bp.seg_begin[1] + nwg + 7) / 8 * 8);
-    body_end = bp.seg_start[1] + (int64_t)(bp.seg_begin[2] - bp.seg_begin[1]);
-  } else {
-    bp.seg_start[1] = bp.seg_begin[1];
-    bp.multi_start = bp.seg_begin[2];
-    body_end = end + nwg;
-  }
+  bp.seg_start[1] = bp.seg_begin[1];
+  bp.multi_start = bp.seg_begin[2];
+  const int64_t body_end = end + nwg;
   // the grid's last segment (measured: placed before the small resolutions it holds 64 slots from
   // ~50 us on and the step is no shorter, 77.4-79.2 vs 77.0-78.0 us)
   bp.q_begin = (int)body_end;
@@ -1569,22 +1555,16 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
   p.band_out = bands_out;
   p.content_out = content_out;
   // scratch: the raw band rows (+ the EMA's spare rows: post.hip post_ema_kernel), the per-frame dtype
-  // flags, then (16-byte aligned) the EMA chunks' warm-up values at their boundaries, end values and
-  // boundary mismatch flags (post_ema_fix_kernel reads the flags as 16-byte vectors)
+  // flags, then (8-byte aligned) the EMA chunks' warm-up values at their boundaries and end values
   const int64_t rows = n_frames + kEmaSpareRows, nch = (n_frames + 63) / 64;
-  const int64_t pre_off = (rows * (c->post.nb + 1) + 3) / 4 * 4;
-  const int64_t nchp = (nch + 15) / 16 * 16;
+  const int64_t pre_off = (rows * (c->post.nb + 1) + 1) / 2 * 2;
   if (c->post.nb) {
-    if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, pre_off + 4 * nch * c->post.nb + nchp * c->post.nb / 4 + 4))
-      return e;
+    if (int e = grow(c, &c->d_post_raw, &c->post_raw_cap, pre_off + 4 * nch * c->post.nb + 4)) return e;
   }
   p.band_raw = c->d_post_raw;
   p.frame64 = reinterpret_cast<int*>(c->d_post_raw + rows * c->post.nb);
   p.ema_pre = reinterpret_cast<double*>(c->d_post_raw + pre_off);
   p.ema_end = p.ema_pre + nch * c->post.nb;
-  p.ema_flag = reinterpret_cast<unsigned char*>(p.ema_end + nch * c->post.nb);
-  if (reinterpret_cast<uintptr_t>(p.ema_flag) % 16 != 0)
-    return fail(c, OMEGA_EHIP, "post scratch: EMA flags not 16-byte aligned");
   HIPC(c, launch_post(p, c->stream));
   if (c->post.nb) {  // the EMA wrote the other state buffer: it is the next call's input
     std::swap(c->post.prev, c->post.prev_out);

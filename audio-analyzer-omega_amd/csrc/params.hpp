@@ -214,9 +214,9 @@ struct MultiPlan {
 //       power limit, so idle slots are not free time. DESIGN.md §8.)
 //   pat: the group order of a two-role segment: 0 alternating groups (each shader engine runs one
 //       role), 1 the period-8 order A B A B B A B A (seen by one XCD through blockIdx % 8, its engines
-//       get the roles in turn, so an engine's short workgroups do not wait behind another's long ones).
-//   seg_start / multi_start: where segment s and the small resolutions begin in the grid (the small
-//       resolutions after segment 1, or between the segments).
+//       get the roles in turn, so an engine's short workgroups do not wait behind another's long
+//       ones; the product's order, round 4: batch kernel 71.3 -> 65.9 us).
+//   seg_start / multi_start / multi_n: where segment s and the small resolutions begin in the grid.
 struct BatchPlan {
   int seg_begin[3];
   int n_roles[2];
@@ -297,8 +297,6 @@ struct PostParams {
   double* ema_pre;             // [n / 64 chunks, nb] scratch: each EMA chunk's warm-up value at the frame
                                // before it (post.hip post_ema_kernel)
   double* ema_end;             // [n / 64 chunks, nb] scratch: each chunk's value at its last frame
-  unsigned char* ema_flag;     // [nb, nchp] scratch: chunk boundary mismatch flags (nchp = chunks
-                               // rounded up to 16)
   int* content_out;            // [n]
   // EMA state {value, float64 dtype, present} in (double-buffered: the kernels read one, write the
   // other)

@@ -295,12 +295,27 @@ constexpr int kEmaBlock = 32;
 static_assert(kEmaBlock <= kEmaSpareRows, "the spare rows cover a block");
 constexpr int kEmaChunk = 64;
 constexpr int kEmaWarm = 256;
+// Grid: 8 x nch x ceil(band groups / 8) workgroups, workgroup w on XCD w % 8 (the hardware's
+// placement): band group g = w % 8 + 8 (w / 8 / nch), chunk w / 8 % nch -- every chunk of a band
+// group runs on one XCD, so the rows the chunks' warm-ups re-read (each raw band row is read by
+// 1 + kEmaWarm / kEmaChunk chunks) come from that XCD's L2 instead of memory.
+__device__ __forceinline__ bool ema_block(const PostParams& p, int& g, int64_t& ch) {
+  const int64_t nch = (p.n + kEmaChunk - 1) / kEmaChunk;
+  const int w = blockIdx.x, slot = w >> 3;
+  g = (w & 7) + 8 * (int)(slot / nch);
+  ch = slot % nch;
+  return g < (p.nb + 63) / 64;
+}
+
 __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
-  const int64_t c0 = (int64_t)blockIdx.y * kEmaChunk;
+  int g;
+  int64_t ch;
+  if (!ema_block(p, g, ch)) return;
+  const int64_t c0 = ch * kEmaChunk;
   if (c0 >= p.n) return;
   // every lane stays (its flag load serves the block's dtype bits); lanes past the last band compute
   // the last band's values and store nothing
-  const int bl = blockIdx.x * 64 + threadIdx.x;
+  const int bl = g * 64 + threadIdx.x;
   const bool live = bl < p.nb;
   const int b = live ? bl : p.nb - 1;
   const EmaCoef k = p.sf[b];
@@ -382,10 +397,10 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
         double last = v[0];
 #pragma unroll
         for (int i = 1; i < kEmaBlock; ++i) last = i < nf ? v[i] : last;
-        p.ema_end[blockIdx.y * (int64_t)p.nb + b] = last;
+        p.ema_end[ch * (int64_t)p.nb + b] = last;
       }
     } else if (f0 + kEmaBlock == c0) {  // the warm-up's value at the frame before this chunk
-      p.ema_pre[blockIdx.y * (int64_t)p.nb + b] = v[kEmaBlock - 1];
+      p.ema_pre[ch * (int64_t)p.nb + b] = v[kEmaBlock - 1];
     }
   }
 }
@@ -396,22 +411,10 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
 // value equals the stored one (from there on the stored values are the recurrence's again: usually a
 // few frames, as the two runs differ by an ulp that the decay drops). A re-run that does not meet the
 // stored values by the chunk's end rewrote that end, so the next chunk is checked against the new
-// value. The checks run in parallel first (post_ema_check_kernel: one flag byte per chunk), then one
-// thread per band re-runs the flagged chunks in order (rare; kFixRun frames loaded at a time) and
-// writes the stream state for the next call.
+// value. One thread per band compares the boundaries of 64 chunks at a time (their ema_pre / ema_end
+// loads issued together), then re-runs the flagged chunks in order (rare; kFixRun frames loaded at a
+// time) and writes the stream state for the next call.
 constexpr int kFixRun = 8;
-
-__global__ __launch_bounds__(64) void post_ema_check_kernel(PostParams p) {
-  const int b = blockIdx.x * 64 + threadIdx.x;
-  const int64_t ch = blockIdx.y;
-  if (b >= p.nb) return;
-  const int64_t nch = (p.n + kEmaChunk - 1) / kEmaChunk, nchp = (nch + 15) / 16 * 16;
-  bool bad = false;
-  // (chunks whose warm-up starts at frame 0 continue the stream exactly)
-  if (ch > kEmaWarm / kEmaChunk && ch < nch)
-    bad = __double_as_longlong(p.ema_pre[ch * p.nb + b]) != __double_as_longlong(p.ema_end[(ch - 1) * p.nb + b]);
-  p.ema_flag[b * nchp + ch] = bad ? 1 : 0;
-}
 
 // re-run chunk frames [f0, f1] from the true value tv (dtype d64) at f0 - 1 until a recomputed value
 // equals the stored one; returns whether it met them (else *last = the rewritten value at f1)
@@ -459,25 +462,21 @@ __global__ __launch_bounds__(64) void post_ema_fix_kernel(PostParams p) {
     // chunks whose warm-up starts at frame 0 continue the stream exactly: the checks start after them
     for (int64_t g0 = kEmaWarm / kEmaChunk + 1; g0 < nch; g0 += 64) {
       const int gn = nch - g0 < 64 ? (int)(nch - g0) : 64;
-      // the group's flag bytes (16 per load) -> one bit per chunk
-      const int64_t nchp = (nch + 15) / 16 * 16;
-      const uint4* fl = reinterpret_cast<const uint4*>(p.ema_flag + b * nchp + (g0 - g0 % 16));
-      const int sh = (int)(g0 % 16);  // (g0 - sh is a multiple of 16; the bits are shifted into place)
-      uint4 q[5];
+      // bit j: chunk g0 + j's warm-up value at its boundary differs from the value there (16 chunks'
+      // loads at a time)
+      unsigned long long mm = 0;
+      for (int j0 = 0; j0 < gn; j0 += 16) {
+        long long pre[16], end[16];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) q[j] = (g0 - sh + 16 * j < nchp) ? fl[j] : make_uint4(0, 0, 0, 0);
-      unsigned long long m80[2] = {0, 0};  // bits of chunks g0 - sh .. g0 - sh + 79
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        const unsigned w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
-#pragma unroll
-        for (int t = 0; t < 16; ++t) {
-          const int bit = 16 * j + t;
-          if ((w[t / 4] >> (8 * (t % 4))) & 0xFFu) m80[bit / 64] |= 1ull << (bit % 64);
+        for (int j = 0; j < 16; ++j) {
+          const int64_t chj = g0 + j0 + j < nch ? g0 + j0 + j : nch - 1;
+          pre[j] = __double_as_longlong(p.ema_pre[chj * nb + b]);
+          end[j] = __double_as_longlong(p.ema_end[(chj - 1) * nb + b]);
         }
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j0 + j < gn && pre[j] != end[j]) mm |= 1ull << (j0 + j);
       }
-      unsigned long long mm = sh ? (m80[0] >> sh) | (m80[1] << (64 - sh)) : m80[0];
-      if (gn < 64) mm &= (1ull << gn) - 1;
       OMEGA_STAMP(11 + g0 / 64);
       int c = -1;  // chunk g0 + c was the last one handled
       while (true) {
@@ -522,10 +521,8 @@ hipError_t launch_post(const PostParams& p, hipStream_t s) {
   if (p.n == 0) return hipSuccess;
   hipLaunchKernelGGL(post_frame_kernel, dim3((unsigned)p.n), dim3(kPostThreads), 0, s, p);
   if (p.nb > 0) {
-    hipLaunchKernelGGL(post_ema_kernel, dim3((p.nb + 63) / 64, (unsigned)((p.n + kEmaChunk - 1) / kEmaChunk)), dim3(64), 0,
-                       s, p);
-    hipLaunchKernelGGL(post_ema_check_kernel, dim3((p.nb + 63) / 64, (unsigned)((p.n + kEmaChunk - 1) / kEmaChunk)),
-                       dim3(64), 0, s, p);
+    const int64_t nch = (p.n + kEmaChunk - 1) / kEmaChunk, ngrp = ((p.nb + 63) / 64 + 7) / 8;
+    hipLaunchKernelGGL(post_ema_kernel, dim3((unsigned)(8 * nch * ngrp)), dim3(64), 0, s, p);
     hipLaunchKernelGGL(post_ema_fix_kernel, dim3((p.nb + 63) / 64), dim3(64), 0, s, p);
   }
   return hipGetLastError();
