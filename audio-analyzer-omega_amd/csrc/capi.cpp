@@ -66,7 +66,10 @@ constexpr int kBatchWaves = 8;  // waves of a batch_kernel workgroup (rfkern.hip
 // most 64 of the 512 batch slots, so at least 192 CUs keep a slot that other roles free as they
 // finish. (Round 1: one meter workgroup per 8 outputs of a 4096-frame batch took every slot and waited
 // until the poll bound expired.)
-constexpr int kMeterWgs = 64;
+#ifndef OMEGA_METER_WGS
+#define OMEGA_METER_WGS 64
+#endif
+constexpr int kMeterWgs = OMEGA_METER_WGS;
 
 
 struct DevBuf {
