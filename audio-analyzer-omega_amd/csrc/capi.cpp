@@ -67,7 +67,7 @@ constexpr int kBatchWaves = 8;  // waves of a batch_kernel workgroup (rfkern.hip
 // finish. (Round 1: one meter workgroup per 8 outputs of a 4096-frame batch took every slot and waited
 // until the poll bound expired.)
 #ifndef OMEGA_METER_WGS
-#define OMEGA_METER_WGS 64
+#define OMEGA_METER_WGS 64  // (measured: 16 and 32 slower, profiles/r04_ab_meter_wgs.txt)
 #endif
 constexpr int kMeterWgs = OMEGA_METER_WGS;
 

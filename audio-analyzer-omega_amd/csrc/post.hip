@@ -462,20 +462,20 @@ __global__ __launch_bounds__(64) void post_ema_fix_kernel(PostParams p) {
     // chunks whose warm-up starts at frame 0 continue the stream exactly: the checks start after them
     for (int64_t g0 = kEmaWarm / kEmaChunk + 1; g0 < nch; g0 += 64) {
       const int gn = nch - g0 < 64 ? (int)(nch - g0) : 64;
-      // bit j: chunk g0 + j's warm-up value at its boundary differs from the value there (16 chunks'
-      // loads at a time)
+      // bit j: chunk g0 + j's warm-up value at its boundary differs from the value there (the group's
+      // 128 loads issued together: one memory latency per 64 chunks; a 64-thread kernel has the VGPRs)
       unsigned long long mm = 0;
-      for (int j0 = 0; j0 < gn; j0 += 16) {
-        long long pre[16], end[16];
+      {
+        long long pre[64], end[64];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int64_t chj = g0 + j0 + j < nch ? g0 + j0 + j : nch - 1;
+        for (int j = 0; j < 64; ++j) {
+          const int64_t chj = g0 + j < nch ? g0 + j : nch - 1;
           pre[j] = __double_as_longlong(p.ema_pre[chj * nb + b]);
           end[j] = __double_as_longlong(p.ema_end[(chj - 1) * nb + b]);
         }
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if (j0 + j < gn && pre[j] != end[j]) mm |= 1ull << (j0 + j);
+        for (int j = 0; j < 64; ++j)
+          if (j < gn && pre[j] != end[j]) mm |= 1ull << j;
       }
       OMEGA_STAMP(11 + g0 / 64);
       int c = -1;  // chunk g0 + c was the last one handled

@@ -62,3 +62,4 @@ def test_meter_prep_model_matches_oracle():
     st = R.MeterState(48000)
     ref = np.array([list(st.update(np.ones(1), float(li[f]), float(tp[f])).values()) for f in range(n)])
     np.testing.assert_allclose(got, ref, rtol=0, atol=1e-9)
+
