@@ -954,7 +954,9 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
     p.wait_ctr = c->d_kw_done;
     p.wait_target = c->kw_issued;
     p.q_done = c->d_kw_done + 3;
+#ifndef OMEGA_PREP_AFTER
     HIPC(c, launch_meter_prep(p, c->fork[0]));
+#endif
     c->prep_issued += (unsigned)p.C;
     mq = mc[0];
     mq.start_ctr = c->d_kw_done + 3;
@@ -968,6 +970,9 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
       (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
       return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
     }
+#ifdef OMEGA_PREP_AFTER
+    HIPC(c, launch_meter_prep(p, c->fork[0]));
+#endif
     c->tp_issued += (unsigned)n;
     return 0;
   }

@@ -51,6 +51,20 @@ __device__ __forceinline__ void meter_roll_tp(const MeterPrepParams& p, int c, i
   }
   if (tid == 0) p.n_t_out[c] = ktl;
 }
+// meter_roll_tp by element e = c HT + i of all channels (the batch's meter workgroups share it): loads
+// element e's value into v and returns its destination, or -1 past the channel's ktl values (the
+// caller stores, so the load can be issued beside the true-peak queries' loads)
+__device__ __forceinline__ int64_t tp_roll_load(const MeterPrepParams& p, int64_t e, float& v) {
+  const int c = (int)(e / p.HT), i = (int)(e % p.HT);
+  const int nt = p.n_t_in[c];
+  const int64_t tt = (int64_t)nt + p.n_frames;
+  const int ktl = (int)min<int64_t>(p.HT, tt);
+  if (i == 0) p.n_t_out[c] = ktl;
+  if (i >= ktl) return -1;
+  const int64_t j = tt - ktl + i;
+  v = j < nt ? p.hist_t_in[(int64_t)c * p.HT + j] : p.tp[(j - nt) * p.C + c];
+  return (int64_t)c * p.HT + i;
+}
 
 // The true-peak meter of output (f, c) in two parts: tp_hist_part -- the window's values from the
 // history (no dependence on this batch's true peaks, so it can run before they are counted in) -- and

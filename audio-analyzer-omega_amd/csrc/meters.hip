@@ -164,7 +164,7 @@ __device__ __forceinline__ void st_wt(MeterExt* q, const MeterExt& e) {
 //   before: stage the sorted history keys A; the CORE = the history's gated values in every window of
 //     the batch (absolute index >= clo = the last frame's window start), sorted -- a compaction of A by
 //     an exclusive in-core prefix cpA; the history part of the time-order gated count / sum prefixes;
-//     the kept prefix over A for the next sorted history; the history part of the next LUFS history.
+//     the kept prefix over A for the next sorted history.
 //   after:  the batch's gated keys, rank-sorted (B); the EXTRAS = the evicted history keys (A minus the
 //     core) merged with B by rank, each with its core count below (cpA at its rank in A); the batch
 //     part of the time-order prefixes; publish (write-through) and count in -- then, off the critical
@@ -259,12 +259,9 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
     // the history's gated totals (the batch part continues from them)
     const int hist_gi = tot.c;
     const double hist_gd = tot.d;
-    // the next LUFS history: its part that comes from this history
+    // (the next LUFS history is written after the count, never here: its buffer is the one the
+    // previous batch's meter segment may still be reading -- this kernel can start while it runs)
     const int klen = min(p.HL, L);
-    for (int i = tid; i < klen; i += 1024) {
-      const int src = L - klen + i;
-      if (src < nh) p.hist_l_out[(int64_t)c * p.HL + i] = p.hist_l_in[(int64_t)c * p.HL + src];
-    }
     // (every index of cpA / kpA below kHistCap is written: the ones at ns and past it hold the totals)
     OMEGA_STAMP(1);
     // ---- the batch's K-weighting values ----
@@ -466,9 +463,12 @@ __global__ __launch_bounds__(1024) void meter_prep_kernel(MeterPrepParams p) {
       const int j = tid * PB + q;
       if (j < Gn && (int64_t)(uint32_t)bk[q] >= thr) S[kbB[j] + kpA[ra[q]]] = bk[q];
     }
+    // the next LUFS history: after the count, i.e. after the batch that counted started, so after every
+    // earlier batch on its stream -- whose meter segment reads this buffer as its history -- ended
     for (int i = tid; i < klen; i += 1024) {
       const int src = L - klen + i;
-      if (src >= nh) p.hist_l_out[(int64_t)c * p.HL + i] = p.lufs[(int64_t)(src - nh) * C + c];
+      p.hist_l_out[(int64_t)c * p.HL + i] =
+          src < nh ? p.hist_l_in[(int64_t)c * p.HL + src] : p.lufs[(int64_t)(src - nh) * C + c];
     }
     if (tid == 0) {
       p.n_s_out[c] = Ka + Kb;

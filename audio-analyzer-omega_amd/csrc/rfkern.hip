@@ -651,7 +651,7 @@ __device__ __forceinline__ void batch_kw_role(const KWeightParams& kp, int64_t c
 // every other role of the batch, so their waits cannot hold back the batch work they wait for: first
 // (bounded) until the meter prep kernel on the side stream has counted in (it has waited for the
 // batch's K-weighting count), then the LUFS meters; then until every true-peak workgroup has counted
-// in, then the true-peak meter (workgroup 0 also rolls the true-peak history). The batch completes only
+// in, then the true-peak meter and the roll of the true-peak history. The batch completes only
 // after both, so the caller's stream needs no join kernel and no stream event. nq is at most
 // kMeterWgs (the host's cap): the waiting workgroups must leave room for the prep kernel, which may be
 // dispatched after them and needs a CU with at most one batch workgroup resident (capi.cpp kMeterWgs).
@@ -671,13 +671,23 @@ __device__ __forceinline__ void batch_meter_role(const MeterPrepParams& mp, int 
   if (tid == 0) poll_count(mp.join_ctr, mp.join_target, mp.poll_limit, mp.err_word + 1);
   __syncthreads();
   OMEGA_MARK(q, 3);
+  // the true-peak history roll, one element per thread of the segment (it writes the other history
+  // buffer, not the one the queries read): its first load issued beside the queries' loads, not
+  // after them in one workgroup (that workgroup ended the batch ~1 us after the others)
+  const int64_t n_roll = (int64_t)mp.C * mp.HT, roll_step = (int64_t)nq * kBatchThreads;
+  int64_t e = (int64_t)q * kBatchThreads + tid;
+  float rv = 0.f;
+  const int64_t rdst = e < n_roll ? tp_roll_load(mp, e, rv) : -1;
   for (int64_t o = o0; o < n_out; o += step) {
     const int64_t f = o / mp.C;
     const int c = (int)(o % mp.C);
     tp_finish(mp, f, c, lane, o == o0 ? th0 : tp_hist_part(mp, f, c, lane));
   }
-  if (q == 0)  // (after the queries: they read the history this replaces in the other buffer only)
-    for (int ch = 0; ch < mp.C; ++ch) meter_roll_tp(mp, ch, tid, kBatchThreads);
+  if (rdst >= 0) mp.hist_t_out[rdst] = rv;
+  for (e += roll_step; e < n_roll; e += roll_step) {
+    const int64_t d = tp_roll_load(mp, e, rv);
+    if (d >= 0) mp.hist_t_out[d] = rv;
+  }
   OMEGA_MARK(q, 4);
 }
 

@@ -713,6 +713,50 @@ def test_many_contexts_default_layout():
                 assert torch.equal(outs[0][r][k], outs[i][r][k]), (i, r, k)
 
 
+def test_unsynchronised_calls_over_a_full_history():
+    """Consecutive device calls with no host synchronisation between them, once the 3599-frame LUFS
+    history is full (so every call's prep shifts it): the next call's meter prep may run while the
+    previous batch's meter segment still reads the history -- the prep must not overwrite the slots the
+    segment reads. Batches shorter and longer than the 30-frame short-term window, bitwise equal to the
+    same calls each followed by a device synchronise, and equal to the oracle's sequential meters."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    rng = np.random.default_rng(33)
+    n0 = 3700
+    li0 = torch.from_numpy(rng.uniform(-60, -10, (n0, 2)).astype(np.float32)).cuda()
+    tp0 = torch.from_numpy(rng.uniform(-30, 0, (n0, 2)).astype(np.float32)).cuda()
+    sizes = [8, 16, 40, 4, 24, 12, 64, 8, 16]
+    x = torch.from_numpy(S.cfg2_batch(sum(sizes), seed_l=8, seed_r=9)).cuda()
+    res = []
+    for sync in (False, True):
+        eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+        eng.meter_update(li0, tp0, n0)
+        torch.cuda.synchronize()
+        if not sync:
+            torch.cuda._sleep(20_000_000)  # (~10 ms: every call below is queued before the first runs)
+        outs, f0 = [], 0
+        for n in sizes:
+            outs.append(eng.process_frames(x[f0:f0 + n], n, 2 * 16384, 16384, combined=False, meters=True))
+            f0 += n
+            if sync:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        eng.synchronize()
+        res.append({k: torch.cat([o[k] for o in outs]).cpu().numpy() for k in outs[0]})
+    for k in res[0]:
+        np.testing.assert_array_equal(res[0][k], res[1][k], err_msg=k)
+    n = sum(sizes)
+    li = res[0]["lufs_inst"].reshape(n, 2)
+    tp = res[0]["true_peak_db"].reshape(n, 2)
+    h_li, h_tp = li0.cpu().numpy(), tp0.cpu().numpy()
+    for c in (0, 1):
+        st = R.MeterState(FS)
+        for f in range(n0):
+            st.update(np.ones(1), float(h_li[f, c]), float(h_tp[f, c]))
+        ref = np.array([list(st.update(np.ones(1), float(li[f, c]), float(tp[f, c])).values()) for f in range(n)])
+        np.testing.assert_allclose(res[0]["meters"].reshape(n, 2, 5)[:, c], ref, rtol=0, atol=1e-9)
+
+
 def test_stream_switch_keeps_meter_order():
     """Calls alternating between two torch streams (omega_set_stream on every call, Engine._bind_stream):
     the switch orders the new stream after the old one, so the meter state carried between calls is

@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--modes", default="0,2,1")
+    ap.add_argument("--no-meters", action="store_true", help="the same calls without the meter aggregates")
     ap.add_argument("--lib", default=None, help="another build in lib/ (A/B of two builds on one box)")
     a = ap.parse_args()
     if a.lib:
@@ -35,22 +36,26 @@ def main():
     bufs = [{"combined": torch.empty(ncf, 512, device="cuda"), "lufs_inst": torch.empty(ncf, device="cuda"),
              "true_peak_db": torch.empty(ncf, device="cuda"),
              "meters": torch.empty(ncf, 5, dtype=torch.float64, device="cuda")} for _ in range(2)]
+    if a.no_meters:
+        for b in bufs:
+            del b["meters"]
     lib = L.lib()
     for mode in (int(m) for m in a.modes.split(",")):
         eng = Engine(NORTHSTAR_RESOLUTIONS, 48000, 20000, target_bins=512, n_channels=2)
         eng._check(lib.omega_set_graphs(eng._ctx, mode))
         for i in range(20):
-            eng.process_frames(x, 256, 2 * 16384, 16384, meters=True, out=bufs[i % 2])
+            eng.process_frames(x, 256, 2 * 16384, 16384, meters=not a.no_meters, out=bufs[i % 2])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(20):
-            eng.process_frames(x, 256, 2 * 16384, 16384, meters=True, out=bufs[i % 2])
+            eng.process_frames(x, 256, 2 * 16384, 16384, meters=not a.no_meters, out=bufs[i % 2])
         th = (time.perf_counter() - t0) / 20 * 1e6
         torch.cuda.synchronize()
         outs = L.Outputs()
         o = bufs[0]
         outs.combined, outs.lufs_inst = o["combined"].data_ptr(), o["lufs_inst"].data_ptr()
-        outs.true_peak_db, outs.meters = o["true_peak_db"].data_ptr(), o["meters"].data_ptr()
+        outs.true_peak_db = o["true_peak_db"].data_ptr()
+        outs.meters = o["meters"].data_ptr() if "meters" in o else None
         t0 = time.perf_counter()
         for i in range(20):
             eng._check(lib.omega_process_frames(eng._ctx, x.data_ptr(), 256, 2 * 16384, 16384, ctypes.byref(outs),
@@ -60,7 +65,7 @@ def main():
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for i in range(a.steps):
-            eng.process_frames(x, 256, 2 * 16384, 16384, meters=True, out=bufs[i % 2])
+            eng.process_frames(x, 256, 2 * 16384, 16384, meters=not a.no_meters, out=bufs[i % 2])
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / a.steps * 1e3

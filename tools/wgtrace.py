@@ -16,7 +16,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from omega_gpu import _lib as _L  # noqa: E402
 
-_L.use_development_library("libomega_trace.so" if "--trace" in sys.argv else "libomega_dev.so")
+_DEV = sys.argv[sys.argv.index("--lib") + 1] if "--lib" in sys.argv else None  # a variant's trace build
+_L.use_development_library(_DEV or ("libomega_trace.so" if "--trace" in sys.argv else "libomega_dev.so"))
 
 ROLE = {0: "kw", 1: "tp", 2: "res16k", 4: "meters", 5: "prep", 20: "spectra", 3 + 512: "res512", 3 + 1024: "res1k", 3 + 2048: "res2k",
         3 + 4096: "res4k", 3 + 8192: "res8k"}
@@ -28,6 +29,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--probe", type=int, default=None, help="trace omega_dev_probe(which) instead of the batch")
     ap.add_argument("--cfg3", action="store_true", help="trace the cfg3 spectra kernel (4096 frames of 8192)")
+    ap.add_argument("--lib", default=None, help="another trace build in lib/ (tools/build_variant.sh ... -DOMEGA_WGTRACE)")
     ap.add_argument("--trace", action="store_true", help="the trace-only build (make trace): product registers")
     ap.add_argument("--meters", action="store_true", help="with the meter aggregates: the prep kernel's and the "
                     "batch meter role's phase marks on the same clock")
