@@ -231,6 +231,18 @@ struct omega_ctx {
   unsigned q_issued = 0;          // LUFS-meter query workgroups launched with the count on (d_kw_done[1])
   unsigned tp_issued = 0;         // batch true-peak workgroups launched with the count on (d_kw_done[2])
   unsigned prep_issued = 0;       // meter prep workgroups launched with the count on (d_kw_done[3])
+  unsigned seg_issued = 0;        // meter-segment workgroups launched (they count in at d_kw_done[4])
+  // seg_issued once the last meter segment that reads parity p's scratch / state has counted in: the
+  // preps' targets before they overwrite them (MeterPrepParams::seg_ctr)
+  unsigned seg_par[2] = {0, 0};
+  // meter pipelining (omega_set_meter_pipelining): the meter segment of the last default-layout batch
+  // with meters, not yet launched -- the next such batch launch runs it first in its grid, any other
+  // use of the meter state (and omega_synchronize / omega_flush_meters) launches it on its own
+  bool pipe = false;
+  bool pend = false;
+  MeterPrepParams pend_mq{};
+  int pend_nq = 0, pend_par = 0;
+  int stage_par = 0;  // pipelined calls alternate the staging of LUFS_inst / TP (the segment reads them later)
   // device-side poll expiry flags (host-mapped: [0] meter prep, [1] join), checked by
   // check_device_err; the poll bound (OMEGA_POLL_LIMIT, a test knob)
   unsigned* h_err = nullptr;
@@ -698,7 +710,9 @@ int build_meter_state(omega_ctx* c) {
     HIPC(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_err), c->h_err, 0));
   }
   HIPC(c, hipMemset(c->d_kw_done, 0, 8 * sizeof(unsigned)));
-  c->kw_issued = c->q_issued = c->tp_issued = c->prep_issued = 0;
+  c->kw_issued = c->q_issued = c->tp_issued = c->prep_issued = c->seg_issued = 0;
+  c->seg_par[0] = c->seg_par[1] = 0;
+  c->pend = false;
   return omega_meter_reset(c);
 }
 
@@ -827,6 +841,9 @@ std::vector<MeterPrepParams> meter_chunks(omega_ctx* c, const float* lufs, const
     p.gsum = c->d_gsum[a];
     p.out = out + f0 * C * OMEGA_N_METERS;
     p.parts = 3;
+    p.seg_ctr = c->d_kw_done + 4;
+    p.seg_pre_target = c->seg_par[a];
+    p.seg_post_target = c->seg_par[b];
     v.push_back(p);
     c->cur = b;
   }
@@ -844,6 +861,27 @@ int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_f
     HIPC(c, launch_meter_query(p, stream));
     first = false;
   }
+  return 0;
+}
+
+// Meter pipelining: the pending meter segment as a launch of its own on the context's stream (the
+// stream of the batch it belongs to: omega_set_stream flushes before switching).
+// Meter pipelining: the pending meter segment as a launch of its own on the context's stream (the
+// stream of the batch it belongs to: omega_set_stream flushes before switching).
+int flush_meters(omega_ctx* c) {
+  if (!c->pend) return 0;
+  HIPC(c, hipSetDevice(c->device));
+  BatchPlan bp{};
+  bp.q_begin = 0;
+  bp.q_n = c->pend_nq;
+  bp.seg_start[0] = bp.seg_start[1] = bp.multi_start = c->pend_nq;  // (no other workgroups)
+  SpectralParams sp{};
+  KWeightParams kp{};
+  const hipError_t le = launch_batch(sp, kp, bp, c->pend_mq, c->pend_nq, c->stream);
+  if (le != hipSuccess) return fail(c, OMEGA_EHIP, "meter segment launch: %s", hipGetErrorString(le));
+  c->pend = false;
+  c->seg_par[c->pend_par] = c->seg_issued + (unsigned)c->pend_nq;
+  c->seg_issued += (unsigned)c->pend_nq;
   return 0;
 }
 
@@ -889,7 +927,7 @@ bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams&
 // joined there (86.2 vs 81.1, round 3). The in-grid meter segment measured even with the query kernels
 // (step 79.4-80.6 vs 79.0-79.4 us) at two fewer launches per call (host enqueue 13-17 vs 22-27 us).
 int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
-                  const float* tp, double* meters, hipStream_t s, int mr, bool do_tp, bool do_kw) {
+                  const float* tp, double* meters, hipStream_t s, int mr, bool do_tp, bool do_kw, bool fold) {
   (void)W;
   const int64_t n = sp.n_cf;
   BatchPlan bp{};
@@ -929,6 +967,11 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   // the per-context scratch and keep the query kernels
   const bool in_grid = meters && do_tp && do_kw && n_frames > 0 && n_frames <= kChunkFrames;
   const int64_t n_mq = in_grid ? std::min<int64_t>((n + kBatchWaves - 1) / kBatchWaves, kMeterWgs) : 0;
+  // meter pipelining (fold): this launch runs the PREVIOUS call's meter segment as its last workgroups
+  // (its inputs are complete: that batch ended before this one starts; the prep that reads this batch's
+  // values still runs beside it on the side stream) and leaves its own pending
+  fold = fold && in_grid;
+  const int64_t q_n = fold ? (c->pend ? c->pend_nq : 0) : n_mq;
   // grid order: segment 0 | segment 1 | small resolutions (measured: the small resolutions between the
   // segments, step 80.4-81.3 vs 76.6-77.5 us, round 4); segment 0 in the period-8 role order
   // (BatchPlan::pat: batch kernel 65.7-66.1 vs 70.9-71.5 us)
@@ -939,41 +982,59 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   bp.multi_start = bp.seg_begin[2];
   const int64_t body_end = end + nwg;
   // the grid's last segment (measured: placed before the small resolutions it holds 64 slots from
-  // ~50 us on and the step is no shorter, 77.4-79.2 vs 77.0-78.0 us)
+  // ~50 us on and the step is no shorter, 77.4-79.2 vs 77.0-78.0 us); pipelined, it waits for nothing
+  // and fills the slots the tail leaves idle (first in the grid it delayed the true peaks: step 68-69
+  // vs 64-65 us without meters)
   bp.q_begin = (int)body_end;
-  bp.q_n = (int)n_mq;
-  const int64_t grid = body_end + n_mq;
+  bp.q_n = (int)q_n;
+  const int64_t grid = body_end + q_n;
   if (grid > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
   MeterPrepParams mq{};
   std::vector<MeterPrepParams> mc;
   if (in_grid) {
+    const int a = c->cur;
+    const unsigned seg_par_was = c->seg_par[a ^ 1];
+    // the pending segment (parity a ^ 1) is enqueued by this launch: the prep's target for the state it
+    // reads (meter_chunks) counts it
+    if (fold && c->pend) c->seg_par[c->pend_par] = c->seg_issued + (unsigned)c->pend_nq;
     mc = meter_chunks(c, lufs, tp, n_frames, meters);
+    // the prep on the side stream, waiting for this batch's K-weighting count
+    MeterPrepParams p = mc[0];
+    p.q_done = c->d_kw_done + 3;
     kp.kw_done = c->d_kw_done;
     c->kw_issued += (unsigned)n;
-    MeterPrepParams p = mc[0];
     p.wait_ctr = c->d_kw_done;
     p.wait_target = c->kw_issued;
-    p.q_done = c->d_kw_done + 3;
-#ifndef OMEGA_PREP_AFTER
     HIPC(c, launch_meter_prep(p, c->fork[0]));
-#endif
     c->prep_issued += (unsigned)p.C;
     mq = mc[0];
     mq.start_ctr = c->d_kw_done + 3;
     mq.start_target = c->prep_issued;
-    sp.tp_done = c->d_kw_done + 2;
-    mq.join_ctr = c->d_kw_done + 2;
-    mq.join_target = c->tp_issued + (unsigned)n;
-    const hipError_t le = launch_batch(sp, kp, bp, mq, (int)grid, s);
+    // the meter segment's wait for the true peaks (each true-peak workgroup stores its value
+    // write-through and counts in); a pipelined segment runs in a later launch, after this batch ended
+    if (!fold) {
+      sp.tp_done = c->d_kw_done + 2;
+      mq.join_ctr = c->d_kw_done + 2;
+      mq.join_target = c->tp_issued + (unsigned)n;
+    }
+    const hipError_t le = launch_batch(sp, kp, bp, fold ? c->pend_mq : mq, (int)grid, s);
     if (le != hipSuccess) {
       // the prep kernel already waits for this batch's count: publish it (see below)
       (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
+      if (fold) c->seg_par[a ^ 1] = seg_par_was;  // (the pending segment stays pending)
       return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
     }
-#ifdef OMEGA_PREP_AFTER
-    HIPC(c, launch_meter_prep(p, c->fork[0]));
-#endif
-    c->tp_issued += (unsigned)n;
+    if (!fold) c->tp_issued += (unsigned)n;
+    if (fold) {
+      if (c->pend) c->seg_issued += (unsigned)c->pend_nq;
+      c->pend = true;
+      c->pend_mq = mq;
+      c->pend_nq = (int)n_mq;
+      c->pend_par = a;
+    } else {
+      c->seg_par[a] = c->seg_issued + (unsigned)n_mq;
+      c->seg_issued += (unsigned)n_mq;
+    }
     return 0;
   }
   if (meters) {
@@ -1020,13 +1081,18 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
 // the true-peak meter after the true peaks on `s`. (Concurrent full-chip kernels lose to this: 512
 // channel-frames are exactly two rounds of 256 CUs, and a CU held by another kernel pushes a third.)
 int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, int64_t n_frames,
-                   const float* lufs, const float* tp, double* meters, hipStream_t s) {
+                   const float* lufs, const float* tp, double* meters, hipStream_t s, bool pipe = false) {
   const bool do_tp = sp.tp_out != nullptr, do_kw = kp.lufs_out || kp.weighted_out;
   const bool do_res = sp.comb_out != nullptr || sp.res[0].mag_out || sp.res[1].mag_out || sp.res[2].mag_out ||
                       sp.res[3].mag_out;
   int mr = -1;
-  if (c->layout == 3 && batch_eligible(c, sp, kp, W, do_res, s, &mr))
-    return enqueue_batch(c, sp, kp, W, n_frames, lufs, tp, meters, s, mr, do_tp, do_kw);
+  const bool batch = c->layout == 3 && batch_eligible(c, sp, kp, W, do_res, s, &mr);
+  // a pending meter segment goes first: folded into this batch's launch when it has an in-grid meter
+  // segment of its own, else on its own
+  const bool fold = pipe && batch && meters && do_tp && do_kw && n_frames > 0 && n_frames <= kChunkFrames;
+  if (c->pend && !fold)
+    if (int e = flush_meters(c)) return e;
+  if (batch) return enqueue_batch(c, sp, kp, W, n_frames, lufs, tp, meters, s, mr, do_tp, do_kw, fold);
   if (do_kw) HIPC(c, launch_kweight(W, kp, s));
   std::vector<MeterPrepParams> mc;
   if (meters) {
@@ -1054,7 +1120,7 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
 
 extern "C" {
 
-const char* omega_version(void) { return "omega-mi355x 0.2 (gfx950, ABI 2)"; }
+const char* omega_version(void) { return "omega-mi355x 0.3 (gfx950, ABI 3)"; }
 
 #ifdef OMEGA_STAMPS
 // Development build only (make dev): one kernel variant over n_cf channel-frames of the context's
@@ -1586,6 +1652,7 @@ int omega_post_process(omega_ctx* c, const float* spectra, int64_t n_frames, int
 void omega_destroy(omega_ctx* c) try {
   if (!c) return;
   if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->pend && !flush_meters(c)) (void)hipStreamSynchronize(c->stream);  // (the last call's meters)
   if (c->own) (void)hipStreamSynchronize(c->own);
   if (c->fork[0]) (void)hipStreamSynchronize(c->fork[0]);
   for (void* p : c->allocs) (void)hipFree(p);
@@ -1612,6 +1679,10 @@ int omega_set_stream(omega_ctx* c, void* s) try {
   if (!c) return OMEGA_EINVAL;
   const hipStream_t ns = static_cast<hipStream_t>(s);  // NULL = the null (default) stream, e.g. torch's
   if (ns != c->stream) {
+    if (c->pend) {  // (a pending meter segment runs on its batch's stream)
+      HIPC(c, hipSetDevice(c->device));
+      if (int e = flush_meters(c)) return e;
+    }
     // The work already enqueued on the old stream -- a batch's meter segment still reading the
     // per-context prep scratch and history, a query kernel -- must finish before the next call's work:
     // on one stream that is stream order, and the next meter prep on fork[0] waits for the next
@@ -1639,6 +1710,10 @@ int omega_get_config(const omega_ctx* c, omega_config* cfg, int* device) {
 
 int omega_set_graphs(omega_ctx* c, int enable) try {
   if (!c) return OMEGA_EINVAL;
+  if (c->pend) {
+    HIPC(c, hipSetDevice(c->device));
+    if (int e = flush_meters(c)) return e;
+  }
   c->use_graph = (enable & 1) != 0;
   // bits 1-2: 0 default (one batch launch where eligible), else the full-chip kernels back to back with
   // the meters on a side stream
@@ -1651,6 +1726,10 @@ int omega_set_graphs(omega_ctx* c, int enable) try {
 
 int omega_synchronize(omega_ctx* c) try {
   if (!c) return OMEGA_EINVAL;
+  if (c->pend) {
+    HIPC(c, hipSetDevice(c->device));
+    if (int e = flush_meters(c)) return e;
+  }
   HIPC(c, hipStreamSynchronize(c->stream));
   return check_device_err(c);
 } catch (...) {
@@ -1659,6 +1738,7 @@ int omega_synchronize(omega_ctx* c) try {
 
 int omega_meter_reset(omega_ctx* c) try {
   if (!c) return OMEGA_EINVAL;
+  if (int e = flush_meters(c)) return e;  // (the pending segment reads the state being reset)
   const int C = c->cfg.n_channels;
   for (int b = 0; b < 2; ++b) {
     HIPC(c, hipMemsetAsync(c->d_nl[b], 0, C * sizeof(int), c->stream));
@@ -1684,6 +1764,11 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
     return fail(c, OMEGA_EINVAL, "frame_stride and channel_stride must be even (8-byte aligned frames)");
   if (ncf > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "too many channel-frames");
   HIPC(c, hipSetDevice(c->device));
+  // meter pipelining applies to direct device-memory calls; any other call runs a pending meter
+  // segment first (before its staging buffers are touched)
+  const bool pipe = c->pipe && mem == OMEGA_MEM_DEVICE && !c->use_graph;
+  if (!pipe)
+    if (int e = flush_meters(c)) return e;
   SpectralParams sp = spectral_params(c);
   sp.frame_stride = frame_stride;
   sp.chan_stride = channel_stride;
@@ -1712,13 +1797,16 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
     for (int r = 0; r < c->cfg.n_res; ++r) mags[r] = out->mag[r];
     if (!aligned8(x)) return fail(c, OMEGA_EINVAL, "input must be 8-byte aligned");
   }
-  // meters need the instantaneous values even when the caller does not ask for them
+  // meters need the instantaneous values even when the caller does not ask for them (pipelined: two
+  // sets of slots in turn, as the meter segment reads them during the next call)
+  const int sl = pipe ? 2 * c->stage_par : 0;
+  if (pipe && meters) c->stage_par ^= 1;
   if (meters && !lufs) {
-    e = stage_buf(c, 10, ncf * sizeof(float), reinterpret_cast<void**>(&lufs));
+    e = stage_buf(c, 10 + sl, ncf * sizeof(float), reinterpret_cast<void**>(&lufs));
     if (e) return e;
   }
   if (meters && !tp) {
-    e = stage_buf(c, 11, ncf * sizeof(float), reinterpret_cast<void**>(&tp));
+    e = stage_buf(c, 11 + sl, ncf * sizeof(float), reinterpret_cast<void**>(&tp));
     if (e) return e;
   }
   sp.x = dx;
@@ -1765,10 +1853,31 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
     if (meters) c->cur ^= (int)(((n_frames + kChunkFrames - 1) / kChunkFrames) & 1);
     return 0;
   }
-  e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->stream);
+  e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->stream, pipe);
   if (e) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
+} catch (...) {
+  return guard_fail(c);
+}
+
+int omega_set_meter_pipelining(omega_ctx* c, int enable) try {
+  if (!c) return OMEGA_EINVAL;
+  if (!enable && c->pend) {
+    HIPC(c, hipSetDevice(c->device));
+    if (int e = flush_meters(c)) return e;
+  }
+  c->pipe = enable != 0;
+  return 0;
+} catch (...) {
+  return guard_fail(c);
+}
+
+int omega_flush_meters(omega_ctx* c) try {
+  if (!c) return OMEGA_EINVAL;
+  if (!c->pend) return 0;
+  HIPC(c, hipSetDevice(c->device));
+  return flush_meters(c);
 } catch (...) {
   return guard_fail(c);
 }
@@ -2059,6 +2168,7 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
   if (n_frames <= 0) return n_frames == 0 ? 0 : fail(c, OMEGA_EINVAL, "negative count");
   if (int e = check_device_err(c)) return e;
   HIPC(c, hipSetDevice(c->device));
+  if (int e = flush_meters(c)) return e;
   const int64_t ncf = n_frames * c->cfg.n_channels;
   std::vector<HostOut> outs;
   const float* dl = lufs_inst;
@@ -2073,6 +2183,10 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
   }
   e = meters_enqueue(c, dl, dt, n_frames, dm, c->stream, nullptr);
   if (e) return e;
+  // the next batch's meter prep runs on the side stream and reads, before its K-weighting count, the
+  // state these kernels write on the caller's stream: order the side stream after them
+  HIPC(c, hipEventRecord(c->ev_fork, c->stream));
+  HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 } catch (...) {

@@ -23,10 +23,12 @@ __device__ __forceinline__ float seq_at(const float* hist, const float* batch, i
   return i < nh ? hist[(int64_t)c * HC + i] : batch[(i - nh) * C + c];
 }
 
-// One lane waits (bounded) until (int)(*ctr - target) >= 0, then acquires at agent scope; on expiry
+// One lane waits (bounded) until (int)(*ctr - target) >= 0, then acquires at agent scope (no counter:
+// no wait); on expiry
 // it stores 1 into *err (host-mapped; reported as OMEGA_EHIP) and goes on. The caller publishes the
 // acquire to the other waves with a barrier.
 __device__ __forceinline__ void poll_count(const unsigned* ctr, unsigned target, int limit, unsigned* err) {
+  if (!ctr) return;  // (ordered by the stream instead)
   bool met = false;
   for (int i = 0; i < limit; ++i) {
     if ((int)(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) {

@@ -148,6 +148,13 @@ struct MeterPrepParams {
   // meter_query_kernel waits (every workgroup, bounded) until (int)(*start_ctr - start_target) >= 0
   unsigned* start_ctr;
   unsigned start_target;
+  // the batch's meter segment (batch_meter_role): when seg_ctr is set every workgroup adds 1 to it
+  // once its reads are done. meter_prep_kernel: before writing the per-batch scratch of its parity it
+  // waits until (int)(*seg_ctr - seg_pre_target) >= 0 (the last segment that reads that scratch is
+  // done), before writing the next state until (int)(*seg_ctr - seg_post_target) >= 0 (the last
+  // segment that reads that state) -- with meter pipelining that segment may run in a later launch
+  unsigned* seg_ctr;
+  unsigned seg_pre_target, seg_post_target;
   // bounded polls: at most poll_limit iterations; on expiry the kernel stores 1 into err_word[0] (prep)
   // or err_word[1] (join) -- host-mapped memory the host checks in omega_synchronize and the next call
   // (OMEGA_EHIP instead of silently stale meters)

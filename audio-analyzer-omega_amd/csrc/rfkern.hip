@@ -688,6 +688,11 @@ __device__ __forceinline__ void batch_meter_role(const MeterPrepParams& mp, int 
     const int64_t d = tp_roll_load(mp, e, rv);
     if (d >= 0) mp.hist_t_out[d] = rv;
   }
+  if (mp.seg_ctr) {  // every read of the scratch and the state is done: the preps may overwrite them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(mp.seg_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   OMEGA_MARK(q, 4);
 }
 
@@ -701,6 +706,7 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
     OMEGA_WG_END(4);
     return;
   }
+
   const int len0 = bp.seg_begin[1], len1 = bp.seg_begin[2] - bp.seg_begin[1];
   const int sg = (b >= bp.seg_start[0] && b < bp.seg_start[0] + len0) ? 0
                  : (b >= bp.seg_start[1] && b < bp.seg_start[1] + len1) ? 1 : -1;

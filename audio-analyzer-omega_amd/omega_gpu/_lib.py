@@ -70,6 +70,8 @@ EXPORTS = {
     "omega_last_error": (C.c_char_p, [C.c_void_p]),
     "omega_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "omega_synchronize": (C.c_int, [C.c_void_p]),
+    "omega_set_meter_pipelining": (C.c_int, [C.c_void_p, C.c_int]),
+    "omega_flush_meters": (C.c_int, [C.c_void_p]),
     "omega_get_stream": (C.c_void_p, [C.c_void_p]),
     "omega_get_config": (C.c_int, [C.c_void_p, C.POINTER(Config), C.POINTER(C.c_int)]),
     "omega_vu_update": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int32, C.c_int64, C.c_int64,
@@ -163,7 +165,10 @@ def lib() -> C.CDLL:
             raise ImportError(f"libomega.so not found at {LIB_PATH}; run `make -C audio-analyzer-omega_amd` "
                               "(or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
+        dev = os.path.basename(LIB_PATH) != "libomega.so"
         for name, (res, args) in EXPORTS.items():
+            if dev and not hasattr(L, name):  # (an older build in an A/B: its ABI's entry points only)
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -119,6 +119,15 @@ class Engine:
     def reset_meters(self):
         self._check(L.lib().omega_meter_reset(self._ctx))
 
+    def set_meter_pipelining(self, enable: bool = True):
+        """omega_set_meter_pipelining: a batch call's meter aggregates are completed by the next batch
+        call's launch (or flush_meters / synchronize) instead of its own (omega.h)."""
+        self._check(L.lib().omega_set_meter_pipelining(self._ctx, int(bool(enable))))
+
+    def flush_meters(self):
+        """Enqueue a pending meter segment on the context's stream (omega_flush_meters)."""
+        self._check(L.lib().omega_flush_meters(self._ctx))
+
     # -- helpers --
     def _alloc(self, like, shape, dtype):
         if _is_torch(like):

@@ -150,8 +150,17 @@ class DeviceBackend:
     def alloc(self, layout):
         return layout.alloc(self.dev)
 
+    # meter pipelining (omega_set_meter_pipelining): each step's launch computes the previous step's
+    # meter aggregates first in its grid; measure() gathers a step's block after the next launch and
+    # flushes the last step's meters inside the timed region
+    pipelined = True
+
     def reset(self):
         self.eng.reset_meters()
+        self.eng.set_meter_pipelining(self.pipelined)
+
+    def flush(self):
+        self.eng.flush_meters()
 
     def process(self, x, frames, out):
         self.eng.process_frames(x, frames, C * W, W, meters=True, out=out)
@@ -182,17 +191,24 @@ def measure(be, rank, world, frames, steps, warmup, gather, seed_base=None, prep
     views = [lay.views(b) for b in bufs]
     pending = [None, None]
     be.reset()
+    # pipelined meters: step i's block is complete once step i + 1's launch (or the flush) is enqueued
+    lag = 1 if getattr(be, "pipelined", False) else 0
 
-    def step(i):
+    def step(i, first):
         b = i % 2
         if pending[b] is not None:
             pending[b].wait()
             pending[b] = None
         be.process(x, frames, views[b])
-        if gather:
-            pending[b] = D.gather_to_root(bufs[b], recv[b], async_op=True)
+        j = i - lag
+        if gather and j >= first:
+            pending[j % 2] = D.gather_to_root(bufs[j % 2], recv[j % 2], async_op=True)
 
-    def drain():
+    def drain(last):
+        if lag:  # the last step's meters, then its gather
+            be.flush()
+            if gather:
+                pending[last % 2] = D.gather_to_root(bufs[last % 2], recv[last % 2], async_op=True)
         for k in range(2):
             if pending[k] is not None:
                 pending[k].wait()
@@ -205,13 +221,14 @@ def measure(be, rank, world, frames, steps, warmup, gather, seed_base=None, prep
         be.sync()
 
     for i in range(warmup):
-        step(i)
-    drain()
+        step(i, 0)
+    if warmup:
+        drain(warmup - 1)
     barrier()
     t0 = time.perf_counter()
     for i in range(warmup, warmup + steps):
-        step(i)
-    drain()
+        step(i, warmup)
+    drain(warmup + steps - 1)
     be.sync()
     t1 = time.perf_counter()
     barrier()
@@ -716,6 +733,10 @@ def main(argv=None):
             "roofline": roof,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
+            "meters": ("pipelined (omega_set_meter_pipelining): each step's meter aggregates are computed by "
+                       "the next step's launch, the last step's by a flush inside the timed region; every "
+                       "step's outputs are complete before the closing synchronize"
+                       if getattr(be, "pipelined", False) else "computed in each step's own launch"),
         }
         if standin:
             line["backend"] = f"stand-in {a.standin} (CPU, {be.dist_backend}); not a measurement"

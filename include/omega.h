@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define OMEGA_ABI_VERSION 2
+#define OMEGA_ABI_VERSION 3
 #define OMEGA_MAX_RES 4
 #define OMEGA_N_METERS 5 /* momentary, short_term, integrated, range, true_peak */
 
@@ -149,7 +149,24 @@ int omega_set_graphs(omega_ctx* ctx, int flags);
 /* The stream calls enqueue on (omega_set_stream), and the context's configuration and device. */
 void* omega_get_stream(const omega_ctx* ctx);
 int omega_get_config(const omega_ctx* ctx, omega_config* cfg, int* device);
+/* Waits for the work enqueued on the context's stream (a pending meter segment launched first). */
 int omega_synchronize(omega_ctx* ctx);
+
+/* Meter pipelining (default off; ABI 3). When on, a direct device-memory omega_process_frames /
+ * omega_process_stream call on the default layout with meters (up to 2048 frames per channel) leaves
+ * its meter aggregates (out->meters) PENDING: the next such call's one batch launch computes them
+ * first in its grid -- their inputs are complete once that batch starts -- instead of this launch
+ * ending with them, so consecutive calls overlap the meters of one with the transforms of the next.
+ * Every other output of a call is complete when its stream work is, as always; its meters are complete
+ * when the stream work of the NEXT call, omega_flush_meters or omega_synchronize is. Any other use of
+ * the meter state (omega_meter_update / omega_meter_reset / omega_calculate_lufs, a host-memory,
+ * graph or other-layout call, omega_set_stream, omega_set_graphs, disabling pipelining,
+ * omega_destroy) launches a pending segment first, on the stream of its batch. The caller keeps the
+ * pending call's meters buffer (and its lufs_inst / true_peak_db buffers, if given) alive until then.
+ * Outputs are bitwise those of the default. */
+int omega_set_meter_pipelining(omega_ctx* ctx, int enable);
+/* Enqueue a pending meter segment now (no-op without one); complete with the stream's work. */
+int omega_flush_meters(omega_ctx* ctx);
 
 /* The fused per-channel-frame hot path over n_frames x n_channels frames of W samples. */
 int omega_process_frames(omega_ctx* ctx, const float* x, int64_t n_frames, int64_t frame_stride,

@@ -13,10 +13,15 @@ FS = 48000
 
 class Backend:
     dist_backend = "gloo"
+    # meter pipelining as the device does it (omega_set_meter_pipelining): a call's meter aggregates
+    # land in its buffer during the NEXT call (or flush), so bench.py's gather of a step must follow the
+    # next step's launch -- a wrong lag shows up as stale meters in the gathered blocks
+    pipelined = True
 
     def __init__(self, local):
         self.dev = torch.device("cpu")
         self.states = {}
+        self.pend = None
 
     def input(self, frames, seed_l, seed_r):
         return torch.from_numpy(S.cfg2_batch(frames, seed_l=seed_l, seed_r=seed_r))
@@ -25,11 +30,21 @@ class Backend:
         return layout.alloc(self.dev)
 
     def reset(self):
+        self.flush()
         self.states = {}
 
+    def flush(self):
+        if self.pend is not None:
+            dst, vals = self.pend
+            dst.copy_(vals)
+            self.pend = None
+
     def process(self, x, frames, out):
+        self.flush()
         xn = x.numpy()
         C = xn.shape[1]
+        met = torch.empty_like(out["meters"])
+        out["meters"].fill_(float("nan"))  # (not yet: the next call writes them)
         for f in range(frames):
             for c in range(C):
                 cf = f * C + c
@@ -38,7 +53,8 @@ class Backend:
                 out["combined"][cf] = torch.from_numpy(np.asarray(comb, np.float32))
                 out["lufs_inst"][cf] = float(li)
                 out["true_peak_db"][cf] = float(tp)
-                out["meters"][cf] = torch.tensor([m[k] for k in R.AGG_KEYS], dtype=torch.float64)
+                met[cf] = torch.tensor([m[k] for k in R.AGG_KEYS], dtype=torch.float64)
+        self.pend = (out["meters"], met)
 
     def sync(self):
         pass

@@ -52,6 +52,31 @@ def test_bench_gpus2_launches_two_ranks_and_gathers(tmp_path):
         buf = lay.alloc()
         be.reset()
         be.process(x, 1, lay.views(buf))
+        be.flush()  # (pipelined meters: the stand-in writes them at the next call or flush, like the device)
+        ref = lay.views(buf)
+        for k in ref:
+            np.testing.assert_array_equal(g[k][2 * rank:2 * rank + 2].numpy(), ref[k].numpy(), err_msg=k)
+
+
+def test_bench_gpus2_pipelined_meters_over_steps(tmp_path):
+    """Several warmup and timed steps: with the stand-in's pipelined meters (written by the next call,
+    like omega_set_meter_pipelining) the last gathered block carries the last step's complete meters --
+    bench.py gathers each step after the next launch and flushes the last one."""
+    from tests.bench_standin import Backend
+    dump = str(tmp_path / "gathered.npy")
+    r = _run(["--gpus", "2", "--steps", "3", "--warmup", "2", "--frames", "1", "--standin", "tests.bench_standin",
+              "--dump", dump], tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lay = D.PackedLayout(2, T)
+    g = D.unpack_gathered([torch.from_numpy(b) for b in np.load(dump)], lay)
+    be = Backend(0)
+    for rank in range(2):
+        x = be.input(1, 2 * rank, 2 * rank + 1)
+        be.reset()
+        for _ in range(5):  # one meter stream over warmup + timed steps
+            buf = lay.alloc()
+            be.process(x, 1, lay.views(buf))
+        be.flush()
         ref = lay.views(buf)
         for k in ref:
             np.testing.assert_array_equal(g[k][2 * rank:2 * rank + 2].numpy(), ref[k].numpy(), err_msg=k)

@@ -757,6 +757,55 @@ def test_unsynchronised_calls_over_a_full_history():
         np.testing.assert_allclose(res[0]["meters"].reshape(n, 2, 5)[:, c], ref, rtol=0, atol=1e-9)
 
 
+def test_meter_pipelining_bitwise():
+    """omega_set_meter_pipelining (omega.h): each batch call's meter aggregates are computed by the next
+    call's launch (or a flush). Over a sequence that mixes pipelined calls of several sizes (one past
+    the 2048-frame chunk: not pipelined, the pending segment runs first), a meter_update and a
+    host-memory call (both flush), a stream switch and an explicit flush, all queued behind a sleep so
+    that every kernel of the sequence is enqueued before the first runs: every output equals the
+    non-pipelined context's bitwise."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    rng = np.random.default_rng(41)
+    sizes = [64, 16, 256, 8, 2100, 32, 128, 4]
+    x = torch.from_numpy(S.cfg2_batch(sum(sizes), seed_l=10, seed_r=11)).cuda()
+    li_u = torch.from_numpy(rng.uniform(-50, -10, (40, 2)).astype(np.float32)).cuda()
+    tp_u = torch.from_numpy(rng.uniform(-20, 0, (40, 2)).astype(np.float32)).cuda()
+    side = torch.cuda.Stream()
+    res = []
+    for pipe in (False, True):
+        eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+        eng.set_meter_pipelining(pipe)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(20_000_000)
+        outs, f0 = [], 0
+        for i, n in enumerate(sizes):
+            xb = x[f0:f0 + n]
+            f0 += n
+            if i == 3:
+                outs.append({"meters": eng.meter_update(li_u, tp_u, 40)})  # (flushes)
+            if i == 5:  # host memory: synchronous, flushes first
+                o = eng.process_frames(xb.cpu().numpy(), n, 2 * 16384, 16384, combined=False, meters=True)
+                outs.append({k: torch.from_numpy(v) for k, v in o.items()})
+                continue
+            if i == 6:
+                with torch.cuda.stream(side):
+                    side.wait_stream(torch.cuda.current_stream())
+                    outs.append(eng.process_frames(xb, n, 2 * 16384, 16384, meters=True))
+                torch.cuda.current_stream().wait_stream(side)
+                continue
+            outs.append(eng.process_frames(xb, n, 2 * 16384, 16384, combined=(i % 2 == 0), meters=True))
+            if i == 1:
+                eng.flush_meters()
+        eng.synchronize()  # (flushes the last call's meters)
+        torch.cuda.synchronize()
+        res.append([{k: v.cpu() for k, v in o.items()} for o in outs])
+    for i, (a, b) in enumerate(zip(*res)):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert torch.equal(a[k], b[k]), (i, k)
+
+
 def test_stream_switch_keeps_meter_order():
     """Calls alternating between two torch streams (omega_set_stream on every call, Engine._bind_stream):
     the switch orders the new stream after the old one, so the meter state carried between calls is

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--modes", default="0,2,1")
     ap.add_argument("--no-meters", action="store_true", help="the same calls without the meter aggregates")
+    ap.add_argument("--pipe", action="store_true", help="meter pipelining (omega_set_meter_pipelining)")
     ap.add_argument("--lib", default=None, help="another build in lib/ (A/B of two builds on one box)")
     a = ap.parse_args()
     if a.lib:
@@ -43,6 +44,8 @@ def main():
     for mode in (int(m) for m in a.modes.split(",")):
         eng = Engine(NORTHSTAR_RESOLUTIONS, 48000, 20000, target_bins=512, n_channels=2)
         eng._check(lib.omega_set_graphs(eng._ctx, mode))
+        if a.pipe:
+            eng.set_meter_pipelining(True)
         for i in range(20):
             eng.process_frames(x, 256, 2 * 16384, 16384, meters=not a.no_meters, out=bufs[i % 2])
         torch.cuda.synchronize()
@@ -66,6 +69,8 @@ def main():
         s.record()
         for i in range(a.steps):
             eng.process_frames(x, 256, 2 * 16384, 16384, meters=not a.no_meters, out=bufs[i % 2])
+        if a.pipe:
+            eng.flush_meters()
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / a.steps * 1e3

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--probe", type=int, default=None, help="trace omega_dev_probe(which) instead of the batch")
     ap.add_argument("--cfg3", action="store_true", help="trace the cfg3 spectra kernel (4096 frames of 8192)")
+    ap.add_argument("--pipe", action="store_true", help="meter pipelining (the previous call's meter segment "
+                    "first in the traced launch)")
     ap.add_argument("--lib", default=None, help="another trace build in lib/ (tools/build_variant.sh ... -DOMEGA_WGTRACE)")
     ap.add_argument("--trace", action="store_true", help="the trace-only build (make trace): product registers")
     ap.add_argument("--meters", action="store_true", help="with the meter aggregates: the prep kernel's and the "
@@ -49,6 +51,8 @@ def main():
     outs.combined, outs.lufs_inst, outs.true_peak_db = (t.data_ptr() for t in keep[:3])
     if a.meters:
         outs.meters = keep[3].data_ptr()
+    if a.pipe:
+        eng.set_meter_pipelining(True)
     if a.probe is not None:
         pf = lib.omega_dev_probe
         pf.restype = C.c_int
