@@ -65,16 +65,29 @@ def main(rnd):
                 j += 1
             runs.append((grids[i], i, j - i))
             i = j
-        i0 = next((runs[k][1] for k in range(1, len(runs)) if runs[k][2] == 23 and runs[k - 1][2] >= steps), None)
+        # round 4 (meter pipelining): the steps' grids carry the PREVIOUS step's meter segment (the first
+        # step after a flush has none) and each phase ends with a flush launch of the segment alone, so the
+        # probe is the first run of 23 equal grids after the pipeline, and the pipeline's 25 step launches
+        # are the dispatches before it with at least the probe's grid (flushes apart)
+        i0 = next((runs[k][1] for k in range(1, len(runs)) if runs[k][2] == 23), None)
         if i0 is not None:
-            pipe, timed = dur[i0 - steps:i0], dur[i0 + 3:i0 + 23]
-            gp, gt = grids[i0 - 1], grids[i0]
+            gt = grids[i0]
+            idx, flush = [], []
+            k = i0 - 1
+            while k >= 0 and len(idx) < steps:
+                (idx if int(grids[k]) >= int(gt) else flush).append(k)
+                k -= 1
+            pipe, timed = [dur[k] for k in idx], dur[i0 + 3:i0 + 23]
+            gp = sorted({grids[k] for k in idx})
             lines += ["", f"Batch kernel `{TP}` (all per-channel-frame work of a step in one launch), cfg2:", "",
-                      f"- in the pipeline (grid {gp}: the step's launch with the meter segment; the meter prep "
-                      f"kernel on the side stream): {len(pipe)} dispatches, avg {sum(pipe) / len(pipe):.1f} us",
+                      f"- in the pipeline (grids {', '.join(gp)}: the step's launch, with the previous step's meter "
+                      f"segment once one is pending; the meter prep kernel on the side stream): {len(pipe)} "
+                      f"dispatches, avg {sum(pipe) / len(pipe):.1f} us",
+                      f"- the meter segment alone (the flush closing the warmup and the timed steps): {len(flush)} "
+                      f"dispatches, avg {sum(dur[k] for k in flush) / max(1, len(flush)):.1f} us",
                       f"- roofline probe (grid {gt}: no meters, back to back; bench.py `roofline.kernel_ms` times "
                       f"these 20 with HIP events): {len(timed)} dispatches, avg {sum(timed) / max(1, len(timed)):.1f} us"]
-            used = set(range(i0 - steps, i0 + 23))
+            used = set(idx) | set(flush) | set(range(i0, i0 + 23))
             others = {}
             for i, r in enumerate(bk):
                 if i not in used:
