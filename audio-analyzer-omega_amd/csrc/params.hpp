@@ -231,6 +231,7 @@ struct BatchPlan {
   int mr_res;
   MultiPlan multi;
   int q_begin, q_n;
+  unsigned* tail_ctr;  // (meter pipelining) the last workgroup adds 1 at its start: see capi.cpp d_tail
   int pat;
   int seg_start[2];
   int multi_start, multi_n;

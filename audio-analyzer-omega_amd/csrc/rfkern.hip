@@ -701,6 +701,10 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
   OMEGA_WG_BEGIN();
+  // meter pipelining: the grid's last workgroup (dispatched last) releases the side stream's wait before
+  // the meter prep (capi.cpp omega_ctx::d_tail)
+  if (bp.tail_ctr && b == (int)gridDim.x - 1 && tid == 0)
+    __hip_atomic_fetch_add(bp.tail_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (b >= bp.q_begin && b < bp.q_begin + bp.q_n) {
     batch_meter_role(mq, b - bp.q_begin, bp.q_n, tid);
     OMEGA_WG_END(4);

@@ -163,7 +163,9 @@ int omega_synchronize(omega_ctx* ctx);
  * graph or other-layout call, omega_set_stream, omega_set_graphs, disabling pipelining,
  * omega_destroy) launches a pending segment first, on the stream of its batch. The caller keeps the
  * pending call's meters buffer (and its lufs_inst / true_peak_db buffers, if given) alive until then.
- * Outputs are bitwise those of the default. */
+ * Outputs are bitwise those of the default. In this mode the batch kernel never waits for the side
+ * stream (the meter prep follows it there behind a stream wait on the batch's last workgroup; only the
+ * next launch's meter segment waits for the prep). */
 int omega_set_meter_pipelining(omega_ctx* ctx, int enable);
 /* Enqueue a pending meter segment now (no-op without one); complete with the stream's work. */
 int omega_flush_meters(omega_ctx* ctx);
