@@ -1767,6 +1767,8 @@ int omega_synchronize(omega_ctx* c) try {
 int omega_meter_reset(omega_ctx* c) try {
   if (!c) return OMEGA_EINVAL;
   if (int e = flush_meters(c)) return e;  // (the pending segment reads the state being reset)
+  // a meter prep on the side stream may still be writing the next state after its count-in
+  if (c->fork[0]) HIPC(c, hipStreamSynchronize(c->fork[0]));
   const int C = c->cfg.n_channels;
   for (int b = 0; b < 2; ++b) {
     HIPC(c, hipMemsetAsync(c->d_nl[b], 0, C * sizeof(int), c->stream));
@@ -2209,6 +2211,10 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
     if (!e) e = stage_out(c, 4, meters, ncf * 5, outs, &dm);
     if (e) return e;
   }
+  // these kernels run on the caller's stream and read the state a meter prep on the side stream may
+  // still be writing (after its count-in): the caller's stream waits for the side stream first
+  HIPC(c, hipEventRecord(c->ev_join[1], c->fork[0]));
+  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[1], 0));
   e = meters_enqueue(c, dl, dt, n_frames, dm, c->stream, nullptr);
   if (e) return e;
   // the next batch's meter prep runs on the side stream and reads, before its K-weighting count, the

@@ -806,6 +806,27 @@ def test_meter_pipelining_bitwise():
             assert torch.equal(a[k], b[k]), (i, k)
 
 
+def test_meter_pipelining_reset_and_destroy_flush():
+    """A pending meter segment completes before omega_meter_reset replaces the state it reads, and at
+    omega_destroy (the context's last call): the meters of both pending calls equal the unpipelined
+    context's bitwise."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    x = torch.from_numpy(S.cfg2_batch(48, seed_l=12, seed_r=13)).cuda()
+    res = []
+    for pipe in (False, True):
+        eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+        eng.set_meter_pipelining(pipe)
+        a = eng.process_frames(x[:32], 32, 2 * 16384, 16384, combined=False, meters=True)
+        eng.reset_meters()  # (flushes a's segment first)
+        b = eng.process_frames(x[32:], 16, 2 * 16384, 16384, combined=False, meters=True)
+        eng.close()  # (flushes b's segment, then waits)
+        torch.cuda.synchronize()
+        res.append((a["meters"].cpu(), b["meters"].cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert torch.isfinite(res[1][1]).all()
+
+
 def test_stream_switch_keeps_meter_order():
     """Calls alternating between two torch streams (omega_set_stream on every call, Engine._bind_stream):
     the switch orders the new stream after the old one, so the meter state carried between calls is
