@@ -60,7 +60,9 @@ struct RegFFT {
   // offset per register (ds_read/ds_write immediate offsets: no per-element address arithmetic):
   //   exchange 1, element (t, k1):       P1 k1 + t   (P1 = P2R: one row per k1 for both exchanges)
   //   exchange 2, element (u, k2, k1):   P2R k1 + P2C k2 + u
-  //   spectrum, frequency n:             a3(n) = n + n/16 (+ 8 for n >= 4096 when K = 8192)
+  //   spectrum, frequency n:             K = 8192: a3(n) = n + n/16 + 8 (n >= 4096); K = 4096: the XOR
+  //                                      swizzle n ^ ((n / 16) mod 16) (the reads of the untangle
+  //                                      conflict-free too: tools/model/regfft_model.py)
   static constexpr int P1 = L == 32 ? 544 : 272;
   static constexpr int P2R = L == 32 ? 544 : 272;
   static constexpr int P2C = L == 32 ? 34 : 17;
@@ -72,26 +74,27 @@ struct RegFFT {
 
   static __device__ __forceinline__ int a3(int n) {
     if constexpr (K == 8192) return n + (n >> 4) + ((n >> 12) << 3);
-    else return n + (n >> 4);
+    else return n ^ ((n >> 4) & 15);
   }
   // bins k = t + NTH r: a3(k) = s3(t) + o3(r)
   static __device__ __forceinline__ int s3(int t) {
-    return t + (t >> 4);
+    if constexpr (K == 8192) return t + (t >> 4);
+    else return t ^ ((t >> 4) & 15);
   }
-  static constexpr int o3(int r) { return K == 8192 ? 544 * r + 8 * (r >> 3) : 272 * r; }
+  static constexpr int o3(int r) { return K == 8192 ? 544 * r + 8 * (r >> 3) : 256 * r; }
   // mirror bins K - t - NTH r, t >= 1: s3m(t) + o3(15 - r) (t = 0: exact except r = 0 (slot K: the
   // callers' slack) and, for K = 8192, r = 8)
   static __device__ __forceinline__ int s3m(int t) { return s3(NTH - t); }
-  // pass-3 output register m of thread s: frequency out_index(s, m), slot s3o(s) + 272 m
+  // pass-3 output register m of thread s: frequency out_index(s, m), slot s3o(s) + o3o(m)
   static __device__ __forceinline__ int out_index(int s, int m) {
     if constexpr (L == 32) return (s >> 5) + 16 * ((s >> 1) & 15) + 256 * (m + 16 * (s & 1));
     else return (s >> 4) + 16 * (s & 15) + 256 * m;
   }
   static __device__ __forceinline__ int s3o(int s) {
     if constexpr (L == 32) return (s >> 5) + 17 * ((s >> 1) & 15) + 4360 * (s & 1);
-    else return (s >> 4) + 17 * (s & 15);
+    else return ((s >> 4) ^ (s & 15)) + 16 * (s & 15);
   }
-  static constexpr int o3o(int m) { return 272 * m; }
+  static constexpr int o3o(int m) { return L == 32 ? 272 * m : 256 * m; }
 
   // v[k] *= w^k, k = 1..15 (powers by a multiply chain)
   static __device__ __forceinline__ void twiddle(float2 (&v)[16], float2 w) {

@@ -25,8 +25,27 @@ def _check(pl, n_slots_max, allowed=("x3m",)):
 
 def test_padded_layouts():
     # (the padded natural-order spectrum reads cost one extra cycle on a few lane groups)
-    _check(M.Plan(4096), 4352, ("x3r", "x3m"))
+    _check(M.Plan(4096), 4352, ("x3m",))
     _check(M.Plan(8192), 8712, ("x3r", "x3m"))
+
+
+def test_natural_order_4096_separable_forms():
+    """RegFFT<4096>'s natural-order slots as the kernel addresses them (regfft.hpp s3 / o3 / s3m / s3o /
+    o3o: a per-thread base plus an immediate offset per register) equal the model's a3 -- the XOR
+    swizzle -- for the untangle's reads, their mirrors and pass 3's stores."""
+    pl = M.Plan(4096)
+    s3 = lambda t: t ^ ((t >> 4) & 15)  # noqa: E731
+    for t in range(256):
+        for r in range(16):
+            assert pl.a3(t + 256 * r) == s3(t) + 256 * r
+            if t:
+                assert pl.a3(4096 - t - 256 * r) == s3(256 - t) + 256 * (15 - r)
+    for s_ in range(256):
+        for m in range(16):
+            assert pl.a3(pl.out_index(s_, m)) == ((s_ >> 4) ^ (s_ & 15)) + 16 * (s_ & 15) + 256 * m
+    # t = 0: the mirror of register r = 0 is bin K (slot 4096, inside the exchange buffer: the callers
+    # take bin 0's real and imaginary parts instead)
+    assert s3(256) + 256 * 15 == 4096 < 4352
 
 
 def test_tight_layout():

@@ -54,7 +54,7 @@ class Plan:
     def a3(self, n):
         if self.K == 8192:
             return n + (n >> 4) + ((n >> 12) << 3)
-        return n + (n >> 4)
+        return n ^ ((n >> 4) & 15)  # (round 4: the padded n + n / 16 left the untangle's reads 2-way)
 
     # ---- thread maps ----
     def p2(self, tau):
