@@ -1023,15 +1023,14 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
       }
     }
     const bool tail = fold && c->tail_ok > 0;
-    if (tail) {
-      bp.tail_ctr = c->d_tail;
-      HIPC(c, hipStreamWaitValue32(c->fork[0], c->d_tail, c->tail_issued + 1, hipStreamWaitValueGte, 0xFFFFFFFFu));
-    }
-    HIPC(c, launch_meter_prep(p, c->fork[0]));
-    c->prep_issued += (unsigned)p.C;
+    if (tail) bp.tail_ctr = c->d_tail;
+    // unpipelined: the prep before the batch (it must be resident while the batch runs: its segment
+    // waits for it); pipelined: after it, behind the stream wait -- enqueued before the batch, a wait
+    // whose stream shared a hardware queue with the batch's would block the batch behind it for ever
+    if (!fold) HIPC(c, launch_meter_prep(p, c->fork[0]));
     mq = mc[0];
     mq.start_ctr = c->d_kw_done + 3;
-    mq.start_target = c->prep_issued;
+    mq.start_target = c->prep_issued + (unsigned)p.C;
     // the meter segment's wait for the true peaks (each true-peak workgroup stores its value
     // write-through and counts in); a pipelined segment runs in a later launch, after this batch ended
     if (!fold) {
@@ -1042,16 +1041,22 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
     const hipError_t le = launch_batch(sp, kp, bp, fold ? c->pend_mq : mq, (int)grid, s);
     if (le != hipSuccess) {
       // the prep kernel already waits for this batch's count: publish it (see below)
-      (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
-      if (tail) {  // (and the side stream's wait for this launch's last workgroup)
-        ++c->tail_issued;
-        (void)hipMemcpy(c->d_tail, &c->tail_issued, sizeof(unsigned), hipMemcpyHostToDevice);
+      if (!fold) {
+        (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
+        c->prep_issued += (unsigned)p.C;
+      } else {
+        c->kw_issued -= (unsigned)n;  // (no prep waits for this launch: nothing was enqueued)
+        c->seg_par[a ^ 1] = seg_par_was;  // (the pending segment stays pending)
       }
-      if (fold) c->seg_par[a ^ 1] = seg_par_was;  // (the pending segment stays pending)
       return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
     }
     if (!fold) c->tp_issued += (unsigned)n;
-    if (tail) ++c->tail_issued;
+    if (tail) {
+      HIPC(c, hipStreamWaitValue32(c->fork[0], c->d_tail, c->tail_issued + 1, hipStreamWaitValueGte, 0xFFFFFFFFu));
+      ++c->tail_issued;
+    }
+    if (fold) HIPC(c, launch_meter_prep(p, c->fork[0]));
+    c->prep_issued += (unsigned)p.C;
     if (fold) {
       if (c->pend) c->seg_issued += (unsigned)c->pend_nq;
       c->pend = true;

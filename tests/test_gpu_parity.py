@@ -689,16 +689,20 @@ def test_time_sharded_stream_meters_on_device():
         prev = D.stream_history(prev[0], prev[1], tails, world)
 
 
-def test_many_contexts_default_layout():
+@pytest.mark.parametrize("pipe", [False, True])
+def test_many_contexts_default_layout(pipe):
     """The default layout's precondition (omega.h, omega_set_stream): the batch kernel and the meter
     prep on the context's side stream must be resident together. Six live contexts (12 streams of
     their own beside torch's, more than the 4 hardware queues a process has) each run the cfg2-shaped
     batch with meters in turn, three rounds: no ordering wait expires and every context gives the same
-    outputs bitwise."""
+    outputs bitwise. With meter pipelining the side stream's stream wait follows the batch it waits
+    for, so streams sharing a hardware queue serialise instead of blocking."""
     import torch
     from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
     x = torch.from_numpy(S.cfg2_batch(32)).cuda()
     engs = [Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2) for _ in range(6)]
+    for e in engs:
+        e.set_meter_pipelining(pipe)
     outs = [[] for _ in engs]
     for _ in range(3):
         for i, e in enumerate(engs):
