@@ -121,8 +121,14 @@ __device__ __forceinline__ void np_leaf_sums_wave(const float* a, int n, float* 
     const int m = len - len % 8;
     float r = 0.f;
     if (live && len >= 8) {
+      // all 15 loads issued before the first add (a leaf has at most 128 elements), the adds in
+      // numpy's order; past the leaf's end the address is clamped and the value not added
       r = b[j];
-      for (int i = 8; i < m; i += 8) r += b[i + j];
+#pragma unroll
+      for (int i = 8; i < 128; i += 8) {
+        const float v = b[min(i, m - 8) + j];
+        if (i < m) r += v;
+      }
     }
     // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) on lane 0 of the group
     r += __shfl_xor(r, 1, 64);

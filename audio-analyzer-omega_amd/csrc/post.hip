@@ -124,6 +124,81 @@ __device__ float select_rank(const float* s, int T, int r, int t, unsigned (*his
   return __uint_as_float(u);
 }
 
+// The percentile of a frame of at most 512 bins whose ranks lie in its top 16 (the 98th percentile
+// up to 512 bins): each wave sorts the order keys of its 128 bins (bitonic network, two keys per lane:
+// key 2l + h on lane l, the distance-1 steps within the lane, the others by DPP / ds_swizzle / one
+// bpermute), keeps its top 16, and every wave merges the four top-16 runs into the frame's top 64 in
+// order -- any key of the frame's top 16 is in its own wave's top 16. No LDS atomics and one barrier
+// instead of the radix select's twelve and the p_hi pass's four.
+template <int M>
+__device__ __forceinline__ unsigned lane_xor(unsigned v) {  // lane l reads lane l ^ M
+  if constexpr (M == 1)
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm 1032
+  else if constexpr (M == 2)
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm 2301
+  else if constexpr (M == 8)
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror 8
+  else if constexpr (M == 32)
+    return (unsigned)__shfl_xor((int)v, 32, 64);
+  else
+    return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (M << 10));  // bitmask mode, xor M
+}
+// compare-exchange with lane l ^ M: the lower lane keeps the smaller key when ascending
+template <int M>
+__device__ __forceinline__ unsigned cas_lane(unsigned x, bool asc) {
+  const unsigned y = lane_xor<M>(x);
+  return (((threadIdx.x & M) == 0) == asc) ? min(x, y) : max(x, y);
+}
+template <int K, int J>
+__device__ __forceinline__ void sort128_pass(unsigned& x0, unsigned& x1, int lane) {
+  const bool asc = ((2 * lane) & K) == 0;  // key e = 2 lane + h ascends where e & K == 0
+  if constexpr (J == 1) {
+    const unsigned lo = min(x0, x1), hi = max(x0, x1);
+    x0 = asc ? lo : hi;
+    x1 = asc ? hi : lo;
+  } else {
+    x0 = cas_lane<J / 2>(x0, asc);
+    x1 = cas_lane<J / 2>(x1, asc);
+    sort128_pass<K, J / 2>(x0, x1, lane);
+  }
+}
+template <int K>
+__device__ __forceinline__ void sort128(unsigned& x0, unsigned& x1, int lane) {
+  sort128_pass<K, K / 2>(x0, x1, lane);
+  if constexpr (K < 128) sort128<K * 2>(x0, x1, lane);
+}
+// the wave's 128 keys of s[128 w ..) (keys past T are 0, below every non-NaN key) sorted; its top 16
+// ascending into top[0 .. 16)
+__device__ __forceinline__ void wave_top16(const float* s, int T, int w, unsigned* top) {
+  const int lane = threadIdx.x & 63, i = 128 * w + 2 * lane;
+  unsigned x0 = i < T ? order_key(s[i]) : 0u, x1 = i + 1 < T ? order_key(s[i + 1]) : 0u;
+  sort128<2>(x0, x1, lane);
+  if (lane >= 56) *reinterpret_cast<uint2*>(top + 2 * (lane - 56)) = make_uint2(x0, x1);
+}
+// the four waves' top-16 runs (top[0 .. 64)) merged: lane l returns the frame's key of rank T - 64 + l
+// (runs 1 and 3 read reversed: two bitonic 32-sequences, merged ascending / descending into one
+// bitonic 64-sequence, merged ascending)
+__device__ __forceinline__ unsigned merge_top64(const unsigned* top) {
+  const int l = threadIdx.x & 63;
+  unsigned x = top[(l & 16) ? (l | 15) - (l & 15) : l];
+  const bool lower = l < 32;
+  x = cas_lane<16>(x, lower);
+  x = cas_lane<8>(x, lower);
+  x = cas_lane<4>(x, lower);
+  x = cas_lane<2>(x, lower);
+  x = cas_lane<1>(x, lower);
+  x = cas_lane<32>(x, true);
+  x = cas_lane<16>(x, true);
+  x = cas_lane<8>(x, true);
+  x = cas_lane<4>(x, true);
+  x = cas_lane<2>(x, true);
+  x = cas_lane<1>(x, true);
+  return x;
+}
+__device__ __forceinline__ float unkey(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
 __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) {
   __shared__ float s[kPostMaxBins];
   __shared__ unsigned hist[2][256];
@@ -159,6 +234,9 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
   if (w == 2 && p.hs < T) m_on = true, m_lo = p.hs, m_n = T - p.hs;
   if (w == 3) m_on = true, m_n = T;
   if (m_on) np_leaf_sums_wave(s + m_lo, m_n, leaves[w]);
+  __shared__ unsigned top[4 * 16];
+  const bool top_sel = T <= 512 && T - 1 - p.p_lo <= 15;
+  if (top_sel) wave_top16(s, T, w, top + 16 * w);  // (published by the barriers below)
   auto fmx = [](float a, float b) { return fmaxf(a, b); };
   float mx = -INFINITY;
   bool nan_here = false;
@@ -192,22 +270,30 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
   // 3) 98th percentile (numpy 'linear', float32): the values of sorted ranks p_lo and p_hi
   // np.max and np.percentile propagate NaN: `nan > 0` is false, no normalisation
   if (mx > 0.f && !has_nan) {
-    const float a = select_rank(s, T, p.p_lo, t, hist, sel);
-    // rank p_hi (= p_lo or p_lo + 1): v_lo again while rank p_hi still holds a copy of it, else the
-    // smallest value above it
-    const unsigned klo = order_key(a);
-    int le = 0;
-    float above = INFINITY;
-    for (int i = t; i < T; i += kPostThreads) {
-      const float v = s[i];
-      if (order_key(v) <= klo)
-        ++le;
-      else
-        above = fminf(above, v);
+    float a, b;
+    if (top_sel) {
+      const unsigned x = merge_top64(top);
+      a = unkey(__shfl(x, 64 - T + p.p_lo, 64));
+      b = unkey(__shfl(x, 64 - T + p.p_hi, 64));
+    } else {
+      a = select_rank(s, T, p.p_lo, t, hist, sel);
+      // rank p_hi (= p_lo or p_lo + 1): v_lo again while rank p_hi still holds a copy of it, else the
+      // smallest value above it
+      const unsigned klo = order_key(a);
+      int le = 0;
+      float above = INFINITY;
+      for (int i = t; i < T; i += kPostThreads) {
+        const float v = s[i];
+        if (order_key(v) <= klo)
+          ++le;
+        else
+          above = fminf(above, v);
+      }
+      le = block_reduce(le, reinterpret_cast<int*>(hist), t, [](int x, int y) { return x + y; });
+      above = block_reduce(above, redf, t, [](float x, float y) { return fminf(x, y); });
+      b = p.p_hi < le ? a : above;
     }
-    le = block_reduce(le, reinterpret_cast<int*>(hist), t, [](int x, int y) { return x + y; });
-    above = block_reduce(above, redf, t, [](float x, float y) { return fminf(x, y); });
-    const float b = p.p_hi < le ? a : above, d = b - a;
+    const float d = b - a;
     // numpy _lerp, no contraction
     const float ref = p.p_g >= 0.5f ? b - d * (1.0f - p.p_g) : a + d * p.p_g;
     if (ref > 0.f)

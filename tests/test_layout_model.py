@@ -82,3 +82,21 @@ def test_meter_prep_model_matches_oracle():
     ref = np.array([list(st.update(np.ones(1), float(li[f]), float(tp[f])).values()) for f in range(n)])
     np.testing.assert_allclose(got, ref, rtol=0, atol=1e-9)
 
+
+
+def test_post_top16_select_model():
+    """The app post-processing's percentile select for frames up to 512 bins (csrc/post.hip
+    wave_top16 / merge_top64, modelled lane for lane in tools/model/post_select_model.py): every wave's
+    128 keys come out sorted and the merged top 64 give np.sort's key at each rank of the top 16, with
+    heavy ties, frames shorter than a wave and frames of one bin."""
+    import post_select_model as P
+    rng = np.random.default_rng(4)
+    for trial in range(400):
+        t = int(rng.integers(1, 513)) if trial > 2 else (1, 16, 512)[trial]
+        keys = rng.integers(1, 2 ** 32 if trial % 2 else 12, size=t).astype(np.uint64)
+        for w in range(4):
+            e, _ = P.wave_top16(keys, w)
+            assert (np.diff(e.astype(np.int64)) >= 0).all()
+        ref = np.sort(keys)
+        for r in range(max(t - 16, 0), t):
+            assert P.select(keys, r) == ref[r], (t, r)
