@@ -125,11 +125,12 @@ __device__ float select_rank(const float* s, int T, int r, int t, unsigned (*his
 }
 
 // The percentile of a frame of at most 512 bins whose ranks lie in its top 16 (the 98th percentile
-// up to 512 bins): each wave sorts the order keys of its 128 bins (bitonic network, two keys per lane:
-// key 2l + h on lane l, the distance-1 steps within the lane, the others by DPP / ds_swizzle / one
-// bpermute), keeps its top 16, and every wave merges the four top-16 runs into the frame's top 64 in
-// order -- any key of the frame's top 16 is in its own wave's top 16. No LDS atomics and one barrier
-// instead of the radix select's twelve and the p_hi pass's four.
+// up to 512 bins), by bitonic folds over the order keys: each wave sorts its 128 keys as 8 runs of 16
+// lanes (two keys per lane: s[128 w + l] ascending, s[128 w + 64 + l] descending), keeps the larger key
+// of each pair (a bitonic run holding the top 16 of the two), and folds the runs by lane xor 16 and 32
+// the same way; every wave then folds the four waves' top-16 runs into the frame's top 16 in order --
+// any key of the frame's top 16 is in its own wave's top 16. No LDS atomics and one barrier instead
+// of the radix select's twelve and the p_hi pass's four.
 template <int M>
 __device__ __forceinline__ unsigned lane_xor(unsigned v) {  // lane l reads lane l ^ M
   if constexpr (M == 1)
@@ -149,51 +150,52 @@ __device__ __forceinline__ unsigned cas_lane(unsigned x, bool asc) {
   const unsigned y = lane_xor<M>(x);
   return (((threadIdx.x & M) == 0) == asc) ? min(x, y) : max(x, y);
 }
-template <int K, int J>
-__device__ __forceinline__ void sort128_pass(unsigned& x0, unsigned& x1, int lane) {
-  const bool asc = ((2 * lane) & K) == 0;  // key e = 2 lane + h ascends where e & K == 0
-  if constexpr (J == 1) {
-    const unsigned lo = min(x0, x1), hi = max(x0, x1);
-    x0 = asc ? lo : hi;
-    x1 = asc ? hi : lo;
-  } else {
-    x0 = cas_lane<J / 2>(x0, asc);
-    x1 = cas_lane<J / 2>(x1, asc);
-    sort128_pass<K, J / 2>(x0, x1, lane);
-  }
+// a bitonic run of 16 lanes sorted (ascending where up)
+__device__ __forceinline__ unsigned bitonic16_merge(unsigned x, bool up) {
+  x = cas_lane<8>(x, up);
+  x = cas_lane<4>(x, up);
+  x = cas_lane<2>(x, up);
+  return cas_lane<1>(x, up);
 }
-template <int K>
-__device__ __forceinline__ void sort128(unsigned& x0, unsigned& x1, int lane) {
-  sort128_pass<K, K / 2>(x0, x1, lane);
-  if constexpr (K < 128) sort128<K * 2>(x0, x1, lane);
-}
-// the wave's 128 keys of s[128 w ..) (keys past T are 0, below every non-NaN key) sorted; its top 16
-// ascending into top[0 .. 16)
-__device__ __forceinline__ void wave_top16(const float* s, int T, int w, unsigned* top) {
-  const int lane = threadIdx.x & 63, i = 128 * w + 2 * lane;
-  unsigned x0 = i < T ? order_key(s[i]) : 0u, x1 = i + 1 < T ? order_key(s[i + 1]) : 0u;
-  sort128<2>(x0, x1, lane);
-  if (lane >= 56) *reinterpret_cast<uint2*>(top + 2 * (lane - 56)) = make_uint2(x0, x1);
-}
-// the four waves' top-16 runs (top[0 .. 64)) merged: lane l returns the frame's key of rank T - 64 + l
-// (runs 1 and 3 read reversed: two bitonic 32-sequences, merged ascending / descending into one
-// bitonic 64-sequence, merged ascending)
-__device__ __forceinline__ unsigned merge_top64(const unsigned* top) {
+// any run of 16 lanes sorted: the 2-, 4- and 8-lane stages alternate by lane bit 2, 4, 8 (flipped for
+// a descending run), then the run's merge
+__device__ __forceinline__ unsigned bitonic16_sort(unsigned x, bool up) {
   const int l = threadIdx.x & 63;
-  unsigned x = top[(l & 16) ? (l | 15) - (l & 15) : l];
-  const bool lower = l < 32;
-  x = cas_lane<16>(x, lower);
-  x = cas_lane<8>(x, lower);
-  x = cas_lane<4>(x, lower);
-  x = cas_lane<2>(x, lower);
-  x = cas_lane<1>(x, lower);
-  x = cas_lane<32>(x, true);
-  x = cas_lane<16>(x, true);
-  x = cas_lane<8>(x, true);
-  x = cas_lane<4>(x, true);
-  x = cas_lane<2>(x, true);
-  x = cas_lane<1>(x, true);
-  return x;
+  bool a = ((l & 2) == 0) == up;
+  x = cas_lane<1>(x, a);
+  a = ((l & 4) == 0) == up;
+  x = cas_lane<2>(x, a);
+  x = cas_lane<1>(x, a);
+  a = ((l & 8) == 0) == up;
+  x = cas_lane<4>(x, a);
+  x = cas_lane<2>(x, a);
+  x = cas_lane<1>(x, a);
+  return bitonic16_merge(x, up);
+}
+// the wave's top 16 of s[128 w .. 128 w + 128) (keys past T are 0, below every non-NaN key) ascending
+// into top[0 .. 16)
+__device__ __forceinline__ void wave_top16(const float* s, int T, int w, unsigned* top) {
+  const int l = threadIdx.x & 63, i = 128 * w + l;
+  unsigned x0 = i < T ? order_key(s[i]) : 0u, x1 = i + 64 < T ? order_key(s[i + 64]) : 0u;
+  x0 = bitonic16_sort(x0, true);
+  x1 = bitonic16_sort(x1, false);
+  unsigned y = max(x0, x1);  // 4 bitonic runs, each the top 16 of its two
+  y = bitonic16_merge(y, (l & 16) == 0);
+  y = max(y, lane_xor<16>(y));
+  y = bitonic16_merge(y, (l & 32) == 0);
+  y = max(y, lane_xor<32>(y));
+  y = bitonic16_merge(y, true);
+  if (l < 16) top[l] = y;
+}
+// the four waves' top-16 runs (top[0 .. 64)) folded: lane l returns the frame's key of rank
+// T - 16 + l % 16 (runs 1 and 3 read reversed, so each pair folds into a bitonic run)
+__device__ __forceinline__ unsigned merge_top16(const unsigned* top) {
+  const int l = threadIdx.x & 63;
+  unsigned y = top[(l & 16) ? (l | 15) - (l & 15) : l];
+  y = max(y, lane_xor<16>(y));
+  y = bitonic16_merge(y, (l & 32) == 0);
+  y = max(y, lane_xor<32>(y));
+  return bitonic16_merge(y, true);
 }
 __device__ __forceinline__ float unkey(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
@@ -272,9 +274,9 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
   if (mx > 0.f && !has_nan) {
     float a, b;
     if (top_sel) {
-      const unsigned x = merge_top64(top);
-      a = unkey(__shfl(x, 64 - T + p.p_lo, 64));
-      b = unkey(__shfl(x, 64 - T + p.p_hi, 64));
+      const unsigned x = merge_top16(top);
+      a = unkey(__shfl(x, 16 - T + p.p_lo, 64));
+      b = unkey(__shfl(x, 16 - T + p.p_hi, 64));
     } else {
       a = select_rank(s, T, p.p_lo, t, hist, sel);
       // rank p_hi (= p_lo or p_lo + 1): v_lo again while rank p_hi still holds a copy of it, else the
