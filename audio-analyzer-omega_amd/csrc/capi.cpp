@@ -1558,6 +1558,21 @@ int omega_drum_features(omega_ctx* c, const float* mag, int64_t n_frames, int32_
   return guard_fail(c);
 }
 
+// The leaves of numpy's pairwise float32 sum over n elements (numpy/_core/src/umath/loops_utils.h.src:
+// up to 128 elements a leaf, above that halves split at a multiple of 8 below n / 2), in the
+// recursion's depth-first order, as offset | length << 16 -- the table post_frame_kernel's range means
+// read instead of walking the recursion per lane (numpy_emul.hpp np_leaf_sums_tab)
+static void np_leaves(int off, int n, int depth, std::vector<unsigned>& out) {
+  if (depth == 0 || n <= 128) {
+    out.push_back((unsigned)off | (unsigned)n << 16);
+    return;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  np_leaves(off, n2, depth - 1, out);
+  np_leaves(off + n2, n - n2, depth - 1, out);
+}
+
 int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, const uint8_t* bass,
                          const float* comp_instr, const float* comp_vocal, const float* vocal_sup,
                          const int32_t* ranges, int32_t p_lo, int32_t p_hi, float p_gamma,
@@ -1611,6 +1626,17 @@ int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, cons
   if (!e) e = up(&dbs, band_start, (size_t)n_bands);
   if (!e) e = up(&dbe, band_end, (size_t)n_bands);
   if (!e) e = up(&dsf, coef.data(), (size_t)n_bands);
+  // the content ranges' leaf tables: [w][0] the count (at most 17 for 2048 bins), [w][1 ..] the leaves
+  std::vector<unsigned> leaf_tab(4 * 32, 0u);
+  const int rn[4] = {p.be, p.ve - p.vs, n_bins - p.hs, n_bins};
+  for (int w = 0; w < 4; ++w) {
+    std::vector<unsigned> lv;
+    np_leaves(0, std::min(std::max(rn[w], 0), n_bins), 6, lv);  // (a range past the bins is not read)
+    leaf_tab[32 * w] = (unsigned)lv.size();
+    for (size_t i = 0; i < lv.size() && i < 31; ++i) leaf_tab[32 * w + 1 + i] = lv[i];
+  }
+  unsigned* dlt = nullptr;
+  if (!e) e = up(&dlt, leaf_tab.data(), leaf_tab.size());
   if (!e) e = dalloc(c, &p.prev, (size_t)std::max(n_bands, 1) * 2);  // two EMA state buffers
   if (!e) e = dalloc(c, &p.has_prev, 4);
   if (e) return e;
@@ -1624,6 +1650,7 @@ int omega_post_configure(omega_ctx* c, int32_t n_bins, const double* curve, cons
   p.bs = dbs;
   p.bend = dbe;
   p.sf = dsf;
+  p.leaf_tab = dlt;
   c->post = p;
   return omega_post_reset(c);
 } catch (...) {

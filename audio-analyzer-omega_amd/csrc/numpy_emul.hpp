@@ -67,21 +67,10 @@ __device__ __forceinline__ float np_mean_f32(const float* a, int n) {
 
 // The same sum computed by one wave (64 lanes), rounding for rounding: numpy's recursion splits the
 // range into leaves of at most 128 elements (depth-first order); 8 lanes per leaf run the leaf's 8
-// interleaved accumulators (lane j: a[j] + a[j+8] + ..., in numpy's order), combined by lane shuffles in
+// interleaved accumulators (lane j: a[j] + a[j+8] + ..., in numpy's order), combined across the lanes in
 // numpy's tree ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), the tail added by the leaf's first lane; lane 0
-// then adds the leaf sums in the recursion's order. n <= 8192 (64 leaves, 8 per pass); ls: 64 floats of
-// the wave's LDS scratch. Every lane returns the sum.
-template <int D>
-__device__ __forceinline__ int np_leaf_count(int n) {
-  if constexpr (D == 0) {
-    return 1;
-  } else {
-    if (n <= 128) return 1;
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    return np_leaf_count<D - 1>(n2) + np_leaf_count<D - 1>(n - n2);
-  }
-}
+// then adds the leaf sums in the recursion's order (np_leaf_combine). The leaves come from a host table
+// (capi.cpp np_leaves): tab[0] the count (<= 31), tab[1 ..] offset | length << 16.
 template <int D>
 __device__ __forceinline__ float np_leaf_combine(int n, const float* ls, int& idx) {
   if constexpr (D == 0) {
@@ -95,29 +84,18 @@ __device__ __forceinline__ float np_leaf_combine(int n, const float* ls, int& id
     return a + b;
   }
 }
-// One wave's share of np_pairwise_sum(a, n) (n <= 8192): the leaf sums, one per leaf in the
-// recursion's depth-first order, into ls[0 .. np_leaf_count(n)) -- 8 lanes per leaf, 8 leaves per pass.
-// The caller publishes ls (a barrier) and combines it with np_leaf_combine on one lane.
-__device__ __forceinline__ void np_leaf_sums_wave(const float* a, int n, float* ls) {
+// One wave's share of np_pairwise_sum(a, n): the leaf sums, one per leaf of the table, into
+// ls[0 .. tab[0]) -- 8 lanes per leaf, 8 leaves per pass. The caller publishes ls (a barrier) and
+// combines it with np_leaf_combine on one lane.
+__device__ __forceinline__ void np_leaf_sums_tab(const float* a, const unsigned* tab, float* ls) {
   const int lane = threadIdx.x & 63, j = lane & 7;
-  const int nl = np_leaf_count<6>(n);
+  const int nl = (int)tab[0];
   for (int l0 = 0; l0 < nl; l0 += 8) {
     const int li = l0 + (lane >> 3);
-    int off = 0, len = n, k = li;
-    for (int d = 0; d < 7 && len > 128; ++d) {  // walk down numpy's splits to leaf li
-      int n2 = len / 2;
-      n2 -= n2 % 8;
-      const int cl = np_leaf_count<6>(n2);
-      if (k < cl) {
-        len = n2;
-      } else {
-        k -= cl;
-        off += n2;
-        len -= n2;
-      }
-    }
     const bool live = li < nl;
-    const float* b = a + off;
+    const unsigned e = live ? tab[1 + li] : 0u;
+    const float* b = a + (e & 0xFFFFu);
+    const int len = (int)(e >> 16);
     const int m = len - len % 8;
     float r = 0.f;
     if (live && len >= 8) {
@@ -130,10 +108,11 @@ __device__ __forceinline__ void np_leaf_sums_wave(const float* a, int n, float* 
         if (i < m) r += v;
       }
     }
-    // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) on lane 0 of the group
-    r += __shfl_xor(r, 1, 64);
-    r += __shfl_xor(r, 2, 64);
-    r += __shfl_xor(r, 4, 64);
+    // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) on lane 0 of the group: quad xor 1 and 2 by
+    // DPP, xor 4 by ds_swizzle
+    r += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r), 0xB1, 0xF, 0xF, false));
+    r += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(r), 0x4E, 0xF, 0xF, false));
+    r += __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(r), 0x1F | (4 << 10)));
     if (live && j == 0) {
       if (len < 8) {
         r = 0.f;

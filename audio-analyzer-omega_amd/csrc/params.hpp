@@ -290,6 +290,7 @@ struct PostParams {
   const float* comp[2];        // [T] frequency compensation: [0] instrumental / bass-heavy, [1] vocal
   const float* vsup;           // [T] vocal-suppression factor (1 outside 800-4000 Hz)
   int be, vs, ve, hs;          // content ranges [0, be), [vs, ve), [hs, T)
+  const unsigned* leaf_tab;    // [4][32] numpy pairwise-sum leaves of the four ranges (capi post configure)
   int p_lo, p_hi;              // 98th percentile: sorted ranks and float32 gamma
   float p_g;
   const int* bs;               // [nb] band starts / ends

@@ -235,10 +235,12 @@ __global__ __launch_bounds__(kPostThreads) void post_frame_kernel(PostParams p) 
   if (w == 1 && p.ve < T) m_on = true, m_lo = p.vs, m_n = p.ve - p.vs;
   if (w == 2 && p.hs < T) m_on = true, m_lo = p.hs, m_n = T - p.hs;
   if (w == 3) m_on = true, m_n = T;
-  if (m_on) np_leaf_sums_wave(s + m_lo, m_n, leaves[w]);
+  if (m_on) np_leaf_sums_tab(s + m_lo, p.leaf_tab + 32 * __builtin_amdgcn_readfirstlane(w), leaves[w]);
+  OMEGA_STAMP(6);
   __shared__ unsigned top[4 * 16];
   const bool top_sel = T <= 512 && T - 1 - p.p_lo <= 15;
   if (top_sel) wave_top16(s, T, w, top + 16 * w);  // (published by the barriers below)
+  OMEGA_STAMP(7);
   auto fmx = [](float a, float b) { return fmaxf(a, b); };
   float mx = -INFINITY;
   bool nan_here = false;
