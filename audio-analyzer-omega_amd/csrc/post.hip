@@ -501,8 +501,8 @@ __global__ __launch_bounds__(64) void post_ema_kernel(PostParams p) {
 // value equals the stored one (from there on the stored values are the recurrence's again: usually a
 // few frames, as the two runs differ by an ulp that the decay drops). A re-run that does not meet the
 // stored values by the chunk's end rewrote that end, so the next chunk is checked against the new
-// value. One thread per band compares the boundaries of 64 chunks at a time (their ema_pre / ema_end
-// loads issued together), then re-runs the flagged chunks in order (rare; kFixRun frames loaded at a
+// value. Four threads per band compare the boundaries of 64 chunks at a time (16 each, their ema_pre /
+// ema_end loads issued together), then the first re-runs the flagged chunks in order (rare; kFixRun frames loaded at a
 // time) and writes the stream state for the next call.
 constexpr int kFixRun = 8;
 
@@ -537,9 +537,14 @@ __device__ __forceinline__ bool ema_rerun(const PostParams& p, int b, int64_t f0
   return false;
 }
 
-__global__ __launch_bounds__(64) void post_ema_fix_kernel(PostParams p) {
-  const int b = blockIdx.x * 64 + threadIdx.x;
-  if (b >= p.nb) return;
+__global__ __launch_bounds__(256) void post_ema_fix_kernel(PostParams p) {
+  // four waves per 64 bands: each loads and compares 16 of a group's 64 chunk boundaries; wave 0 then
+  // re-runs the flagged chunks and writes the state
+  __shared__ unsigned long long part_mm[4][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int bl = blockIdx.x * 64 + lane;
+  const bool live = bl < p.nb;
+  const int b = live ? bl : p.nb - 1;
   const EmaCoef k = p.sf[b];
   const bool smooth = (p.flags & 8) != 0;
   const int64_t n = p.n, nb = p.nb;
@@ -552,21 +557,27 @@ __global__ __launch_bounds__(64) void post_ema_fix_kernel(PostParams p) {
     // chunks whose warm-up starts at frame 0 continue the stream exactly: the checks start after them
     for (int64_t g0 = kEmaWarm / kEmaChunk + 1; g0 < nch; g0 += 64) {
       const int gn = nch - g0 < 64 ? (int)(nch - g0) : 64;
-      // bit j: chunk g0 + j's warm-up value at its boundary differs from the value there (the group's
-      // 128 loads issued together: one memory latency per 64 chunks; a 64-thread kernel has the VGPRs)
-      unsigned long long mm = 0;
+      // bit j: chunk g0 + j's warm-up value at its boundary differs from the value there (each wave's
+      // 32 loads issued together)
       {
-        long long pre[64], end[64];
+        unsigned long long part = 0;
+        long long pre[16], end[16];
 #pragma unroll
-        for (int j = 0; j < 64; ++j) {
+        for (int i = 0; i < 16; ++i) {
+          const int j = 16 * q + i;
           const int64_t chj = g0 + j < nch ? g0 + j : nch - 1;
-          pre[j] = __double_as_longlong(p.ema_pre[chj * nb + b]);
-          end[j] = __double_as_longlong(p.ema_end[(chj - 1) * nb + b]);
+          pre[i] = __double_as_longlong(p.ema_pre[chj * nb + b]);
+          end[i] = __double_as_longlong(p.ema_end[(chj - 1) * nb + b]);
         }
 #pragma unroll
-        for (int j = 0; j < 64; ++j)
-          if (j < gn && pre[j] != end[j]) mm |= 1ull << j;
+        for (int i = 0; i < 16; ++i)
+          if (16 * q + i < gn && pre[i] != end[i]) part |= 1ull << (16 * q + i);
+        part_mm[q][lane] = live ? part : 0ull;  // (lanes past the last band re-run nothing)
       }
+      __syncthreads();
+      unsigned long long mm = part_mm[0][lane] | part_mm[1][lane] | part_mm[2][lane] | part_mm[3][lane];
+      __syncthreads();  // (the next group's masks overwrite these)
+      if (q != 0) continue;
       OMEGA_STAMP(11 + g0 / 64);
       int c = -1;  // chunk g0 + c was the last one handled
       while (true) {
@@ -597,6 +608,7 @@ __global__ __launch_bounds__(64) void post_ema_fix_kernel(PostParams p) {
   OMEGA_STAMP_AT(22, (unsigned long long)__popcll(__ballot(reruns >= 2)));
   OMEGA_STAMP_AT(23, (unsigned long long)__popcll(__ballot(reruns >= 4)));
   (void)reruns;
+  if (q != 0 || !live) return;
   p.prev_out[b] = p.band_out[(n - 1) * nb + b];
   if (b == 0) {
     p.has_prev_out[0] = 1;
@@ -613,7 +625,7 @@ hipError_t launch_post(const PostParams& p, hipStream_t s) {
   if (p.nb > 0) {
     const int64_t nch = (p.n + kEmaChunk - 1) / kEmaChunk, ngrp = ((p.nb + 63) / 64 + 7) / 8;
     hipLaunchKernelGGL(post_ema_kernel, dim3((unsigned)(8 * nch * ngrp)), dim3(64), 0, s, p);
-    hipLaunchKernelGGL(post_ema_fix_kernel, dim3((p.nb + 63) / 64), dim3(64), 0, s, p);
+    hipLaunchKernelGGL(post_ema_fix_kernel, dim3((p.nb + 63) / 64), dim3(256), 0, s, p);
   }
   return hipGetLastError();
 }
