@@ -1004,6 +1004,7 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
     // the pending segment (parity a ^ 1) is enqueued by this launch: the prep's target for the state it
     // reads (meter_chunks) counts it
     if (fold && c->pend) c->seg_par[c->pend_par] = c->seg_issued + (unsigned)c->pend_nq;
+    const int cur_was = c->cur;  // (meter_chunks flips the state parity)
     mc = meter_chunks(c, lufs, tp, n_frames, meters);
     // the prep on the side stream, waiting for this batch's K-weighting count
     MeterPrepParams p = mc[0];
@@ -1047,6 +1048,7 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
       } else {
         c->kw_issued -= (unsigned)n;  // (no prep waits for this launch: nothing was enqueued)
         c->seg_par[a ^ 1] = seg_par_was;  // (the pending segment stays pending)
+        c->cur = cur_was;                 // (no prep writes the other parity's state)
       }
       return fail(c, OMEGA_EHIP, "batch launch: %s", hipGetErrorString(le));
     }
@@ -1112,8 +1114,10 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
 // workgroups per channel: latency-bound) run on fork[0] beside the resolution and true-peak kernels,
 // the true-peak meter after the true peaks on `s`. (Concurrent full-chip kernels lose to this: 512
 // channel-frames are exactly two rounds of 256 CUs, and a CU held by another kernel pushes a third.)
-int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& kp, int W, int64_t n_frames,
-                   const float* lufs, const float* tp, double* meters, hipStream_t s, bool pipe = false) {
+// lufs_st / tp_st: the context's staging slots of a pipelined call with meters (omega_process_frames).
+int enqueue_frames(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int64_t n_frames, const float* lufs,
+                   const float* tp, double* meters, hipStream_t s, bool pipe = false, float* lufs_st = nullptr,
+                   float* tp_st = nullptr) {
   const bool do_tp = sp.tp_out != nullptr, do_kw = kp.lufs_out || kp.weighted_out;
   const bool do_res = sp.comb_out != nullptr || sp.res[0].mag_out || sp.res[1].mag_out || sp.res[2].mag_out ||
                       sp.res[3].mag_out;
@@ -1124,6 +1128,15 @@ int enqueue_frames(omega_ctx* c, const SpectralParams& sp, const KWeightParams& 
   const bool fold = pipe && batch && meters && do_tp && do_kw && n_frames > 0 && n_frames <= kChunkFrames;
   if (c->pend && !fold)
     if (int e = flush_meters(c)) return e;
+  if (fold && lufs_st && tp_st) {
+    // the segment and the prep read the staging slots; the caller's buffers get copies
+    if (kp.lufs_out != lufs_st) kp.lufs_copy = kp.lufs_out;
+    if (sp.tp_out != tp_st) sp.tp_copy = sp.tp_out;
+    kp.lufs_out = lufs_st;
+    sp.tp_out = tp_st;
+    lufs = lufs_st;
+    tp = tp_st;
+  }
   if (batch) return enqueue_batch(c, sp, kp, W, n_frames, lufs, tp, meters, s, mr, do_tp, do_kw, fold);
   if (do_kw) HIPC(c, launch_kweight(W, kp, s));
   std::vector<MeterPrepParams> mc;
@@ -1859,17 +1872,24 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
     for (int r = 0; r < c->cfg.n_res; ++r) mags[r] = out->mag[r];
     if (!aligned8(x)) return fail(c, OMEGA_EINVAL, "input must be 8-byte aligned");
   }
-  // meters need the instantaneous values even when the caller does not ask for them (pipelined: two
-  // sets of slots in turn, as the meter segment reads them during the next call)
+  // meters need the instantaneous values even when the caller does not ask for them. Pipelined, the
+  // meter prep and the deferred meter segment read them during the next call, so they read the
+  // context's staging slots (two sets in turn) and never the caller's buffers, which the next call may
+  // overwrite (the usual preallocated outputs): enqueue_frames points the batch's K-weighting and
+  // true-peak roles at the slots and hands them the caller's buffers as copies.
   const int sl = pipe ? 2 * c->stage_par : 0;
   if (pipe && meters) c->stage_par ^= 1;
-  if (meters && !lufs) {
-    e = stage_buf(c, 10 + sl, ncf * sizeof(float), reinterpret_cast<void**>(&lufs));
+  float* lufs_st = nullptr;
+  float* tp_st = nullptr;
+  if (meters && (pipe || !lufs)) {
+    e = stage_buf(c, 10 + sl, ncf * sizeof(float), reinterpret_cast<void**>(&lufs_st));
     if (e) return e;
+    if (!lufs) lufs = lufs_st;
   }
-  if (meters && !tp) {
-    e = stage_buf(c, 11 + sl, ncf * sizeof(float), reinterpret_cast<void**>(&tp));
+  if (meters && (pipe || !tp)) {
+    e = stage_buf(c, 11 + sl, ncf * sizeof(float), reinterpret_cast<void**>(&tp_st));
     if (e) return e;
+    if (!tp) tp = tp_st;
   }
   sp.x = dx;
   sp.comb_out = comb;
@@ -1915,8 +1935,11 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
     if (meters) c->cur ^= (int)(((n_frames + kChunkFrames - 1) / kChunkFrames) & 1);
     return 0;
   }
-  e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->stream, pipe);
-  if (e) return e;
+  e = enqueue_frames(c, sp, kp, W, n_frames, lufs, tp, meters, c->stream, pipe, lufs_st, tp_st);
+  if (e) {
+    if (pipe && meters) c->stage_par ^= 1;  // (a still-pending segment reads the slots of the other parity)
+    return e;
+  }
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 } catch (...) {

@@ -251,13 +251,16 @@ __device__ __forceinline__ void gather_edges(const float (&u)[L], float* e, int 
 
 // LUFS_inst store of thread 0. PUB: write-through (sc1) agent-scope store, so that a counter add
 // after this thread's vmcnt drain publishes it to a consumer on another CU / XCD (batch_kernel).
+// With PUB, the caller's buffer (KWeightParams::lufs_copy, meter pipelining) gets a plain copy.
 template <bool PUB>
-__device__ __forceinline__ void put_lufs(float* o, int64_t cf, float v) {
-  if constexpr (PUB)
-    __hip_atomic_store(reinterpret_cast<unsigned*>(o + cf), __float_as_uint(v), __ATOMIC_RELAXED,
+__device__ __forceinline__ void put_lufs(const KWeightParams& p, int64_t cf, float v) {
+  if constexpr (PUB) {
+    __hip_atomic_store(reinterpret_cast<unsigned*>(p.lufs_out + cf), __float_as_uint(v), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-  else
-    o[cf] = v;
+    if (p.lufs_copy) p.lufs_copy[cf] = v;
+  } else {
+    p.lufs_out[cf] = v;
+  }
 }
 
 // After kweight_body<..., PUB = true>: thread 0 stored the value write-through; drain, then count in.
@@ -314,12 +317,12 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
   if (p.mode == 3) {  // Z-weighting: the signal itself, no gate
     if (wout) static_for<0, L>([&](auto i) { wout[i] = u[i]; });
     if (tid == 0 && p.lufs_out)
-      put_lufs<PUB>(p.lufs_out, cf, ms_in > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms_in)) : -100.0f);
+      put_lufs<PUB>(p, cf, ms_in > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms_in)) : -100.0f);
     return;
   }
   if (sqrt(ms_in) < 1e-6) {  // professional_meters.py:132-134
     if (wout) static_for<0, L>([&](auto i) { wout[i] = 0.f; });
-    if (tid == 0 && p.lufs_out) put_lufs<PUB>(p.lufs_out, cf, -100.0f);
+    if (tid == 0 && p.lufs_out) put_lufs<PUB>(p, cf, -100.0f);
     return;
   }
   // Filter x - c instead of x, c = the frame's float32 mean: K(x) = K(x - c) exactly (filtfilt is
@@ -364,7 +367,7 @@ __device__ __forceinline__ void kweight_body(const KWeightParams& p, int64_t cf,
     }
   }
   const double ms = block_sum_f<NTH>(acc, red, tid) / M;
-  if (tid == 0 && p.lufs_out) put_lufs<PUB>(p.lufs_out, cf, ms > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms)) : -100.0f);
+  if (tid == 0 && p.lufs_out) put_lufs<PUB>(p, cf, ms > 1e-10 ? (float)(-0.691 + 10.0 * log10(ms)) : -100.0f);
   OMEGA_STAMP(26);
 }
 

@@ -52,6 +52,9 @@ struct SpectralParams {
   // batch_kernel's true-peak role: when set, the value is stored write-through and the workgroup adds 1
   // after it (the true-peak meter query on the side stream waits for the batch's count)
   unsigned* tp_done;
+  // batch_kernel's true-peak role with meter pipelining: tp_out is the context's staging slot the
+  // deferred meter segment reads, and the caller's buffer (when given) gets this copy
+  float* tp_copy;
 };
 
 // One zero-phase biquad (filtfilt with scipy's defaults) in state-space form:
@@ -85,6 +88,9 @@ struct KWeightParams {
   // when set: LUFS_inst is stored write-through and each workgroup adds 1 after it (the meter prep
   // kernel on the side stream waits for the batch's count instead of a stream event)
   unsigned* kw_done;
+  // batch_kernel with meter pipelining: lufs_out is the context's staging slot the meter prep and the
+  // deferred segment read, and the caller's buffer (when given) gets this copy
+  float* lufs_copy;
 };
 
 // Meter aggregates (meters.hip): per-channel double-buffered state (in -> out) plus per-batch scratch.

@@ -165,6 +165,7 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
     } else {
       p.tp_out[cf] = db;
     }
+    if (p.tp_copy) p.tp_copy[cf] = db;  // (meter pipelining: tp_out is the context's staging slot)
   }
 }
 

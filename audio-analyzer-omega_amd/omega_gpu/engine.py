@@ -77,6 +77,11 @@ class Engine:
         self.W, self.C, self.T = cfg.frame_size, cfg.n_channels, cfg.target_bins
         self.device = device
         self._ingests = []  # weak references: stream ingests bound to this context, closed before it
+        # meter pipelining: the outputs of the last pipelined device call, held until its deferred meter
+        # segment is enqueued (the next call, a flush, synchronize, reset or close): the segment writes
+        # that call's meters, so their memory must not return to torch's caching allocator before then
+        self._pipe = False
+        self._held = None
         code = lib.omega_create(C.byref(cfg), int(device), C.byref(self._ctx))
         if code != L.OK:
             msg = lib.omega_last_error(self._ctx).decode()
@@ -95,6 +100,7 @@ class Engine:
         if self._ctx:
             L.lib().omega_destroy(self._ctx)
             self._ctx = C.c_void_p()
+        self._held = None
 
     def __del__(self):
         try:
@@ -107,6 +113,7 @@ class Engine:
 
     def synchronize(self):
         self._check(L.lib().omega_synchronize(self._ctx))
+        self._held = None
 
     def _bind_stream(self, tensor):
         """Enqueue on torch's current stream of the tensor's device, which must be this context's GPU
@@ -118,15 +125,20 @@ class Engine:
 
     def reset_meters(self):
         self._check(L.lib().omega_meter_reset(self._ctx))
+        self._held = None  # (the reset enqueued a pending segment first)
 
     def set_meter_pipelining(self, enable: bool = True):
         """omega_set_meter_pipelining: a batch call's meter aggregates are completed by the next batch
         call's launch (or flush_meters / synchronize) instead of its own (omega.h)."""
         self._check(L.lib().omega_set_meter_pipelining(self._ctx, int(bool(enable))))
+        self._pipe = bool(enable)
+        if not enable:
+            self._held = None
 
     def flush_meters(self):
         """Enqueue a pending meter segment on the context's stream (omega_flush_meters)."""
         self._check(L.lib().omega_flush_meters(self._ctx))
+        self._held = None
 
     # -- helpers --
     def _alloc(self, like, shape, dtype):
@@ -186,6 +198,9 @@ class Engine:
         else:
             self._check(L.lib().omega_process_frames(self._ctx, _ptr(x), int(n_frames), int(frame_stride),
                                                      int(channel_stride), C.byref(outs), mem))
+        # the previous pipelined call's segment is enqueued by now (this call, or the flush a non-pipelined
+        # call runs first); this call's may be pending: hold its outputs (see __init__)
+        self._held = o if (self._pipe and dev and meters) else None
         return o
 
     def combine(self, mags: Dict[int, np.ndarray], n_cf: int = 1) -> np.ndarray:

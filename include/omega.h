@@ -162,7 +162,10 @@ int omega_synchronize(omega_ctx* ctx);
  * the meter state (omega_meter_update / omega_meter_reset / omega_calculate_lufs, a host-memory,
  * graph or other-layout call, omega_set_stream, omega_set_graphs, disabling pipelining,
  * omega_destroy) launches a pending segment first, on the stream of its batch. The caller keeps the
- * pending call's meters buffer (and its lufs_inst / true_peak_db buffers, if given) alive until then.
+ * pending call's meters buffer alive and unwritten until then (the segment writes it). The segment
+ * and the meter prep read the batch's LUFS_inst / true-peak values from the context's own staging
+ * (two sets in turn), never from the caller's lufs_inst / true_peak_db buffers, which are free to be
+ * reused by the next call as soon as this call's stream work completes (they receive copies).
  * Outputs are bitwise those of the default. In this mode the batch kernel never waits for the side
  * stream (the meter prep follows it there behind a stream wait on the batch's last workgroup; only the
  * next launch's meter segment waits for the prep). */

@@ -832,6 +832,66 @@ def test_meter_pipelining_reset_and_destroy_flush():
     assert torch.isfinite(res[1][1]).all()
 
 
+def test_meter_pipelining_reused_output_buffers():
+    """with pipelining, call N's meter prep and deferred segment run during call N + 1. The
+    caller's preallocated lufs_inst / true_peak_db / combined buffers, passed again to every call, are
+    overwritten by call N + 1's batch while they run -- so they read the context's staging slots, not
+    those buffers. Consecutive calls on one out dict (fresh meters per call, as omega.h asks), queued
+    behind a sleep: meters bitwise equal to the unpipelined context's, and the shared buffers hold the
+    last call's values."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    nb, n = 6, 32
+    x = torch.from_numpy(S.cfg2_batch(nb * n, seed_l=14, seed_r=15)).cuda()
+    x[n:2 * n] *= 0.25  # (batches of distinct loudness: a segment reading the wrong batch differs)
+    res = []
+    for pipe in (False, True):
+        eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+        eng.set_meter_pipelining(pipe)
+        shared = {"combined": torch.empty(2 * n, 512, device="cuda"), "lufs_inst": torch.empty(2 * n, device="cuda"),
+                  "true_peak_db": torch.empty(2 * n, device="cuda")}
+        torch.cuda.synchronize()
+        torch.cuda._sleep(20_000_000)
+        mets = []
+        for b in range(nb):
+            o = dict(shared, meters=torch.empty(2 * n, 5, dtype=torch.float64, device="cuda"))
+            mets.append(eng.process_frames(x[b * n:(b + 1) * n], n, 2 * 16384, 16384, meters=True, out=o)["meters"])
+        eng.synchronize()
+        torch.cuda.synchronize()
+        res.append(([m.cpu() for m in mets], {k: v.cpu() for k, v in shared.items()}))
+    for b in range(nb):
+        assert torch.equal(res[0][0][b], res[1][0][b]), b
+    for k in res[0][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
+
+
+def test_meter_pipelining_discarded_outputs():
+    """the facade's default outputs of a pipelined call, all but meters discarded at once
+    (``m = eng.process_frames(...)['meters']`` in a loop): torch's caching allocator hands the freed
+    blocks to the next call, which writes them while the previous call's meters are still pending --
+    harmless, since the pending work reads only the context's staging and writes the meters the caller
+    keeps (Engine holds the pending call's outputs until its segment is enqueued). Bitwise equal to the
+    unpipelined context."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    nb, n = 5, 16
+    x = torch.from_numpy(S.cfg2_batch(nb * n, seed_l=16, seed_r=17)).cuda()
+    x[2 * n:3 * n] *= 3.0
+    res = []
+    for pipe in (False, True):
+        eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+        eng.set_meter_pipelining(pipe)
+        torch.cuda.synchronize()
+        torch.cuda._sleep(20_000_000)
+        mets = [eng.process_frames(x[b * n:(b + 1) * n], n, 2 * 16384, 16384, meters=True)["meters"]
+                for b in range(nb)]
+        eng.synchronize()
+        torch.cuda.synchronize()
+        res.append([m.cpu() for m in mets])
+    for b in range(nb):
+        assert torch.equal(res[0][b], res[1][b]), b
+
+
 def test_stream_switch_keeps_meter_order():
     """Calls alternating between two torch streams (omega_set_stream on every call, Engine._bind_stream):
     the switch orders the new stream after the old one, so the meter state carried between calls is

@@ -92,12 +92,15 @@ def main():
         run()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_begin = time.time()
     s.record()
     for _ in range(a.reps):
         run()
     e.record()
     torch.cuda.synchronize()
+    t_end = time.time()
     us = s.elapsed_time(e) / a.reps * 1e3
+    print(f"window {t_begin:.3f} {t_end:.3f}")
     print(f"{a.stage}: {us:.1f} us per call, {us * 1e3 / ncf:.1f} ns per channel-frame ({ncf} cf)" +
           (f" = {ncf / us * 1e6:.0f} channel-frames/s (host in/out)" if a.stage == "host" else ""))
 
