@@ -274,6 +274,7 @@ struct omega_ctx {
   float* d_wgt[kMaxRes] = {};
   CombEnt* d_ent = nullptr;
   int ent_begin[kMaxRes] = {}, ent_end[kMaxRes] = {};
+  int pair_lo[kMaxRes] = {}, pair_hi[kMaxRes] = {};  // ResParam::pair_lo / pair_hi
   int ent_jmax[kMaxRes] = {};  // the highest bin a resolution's combine entries read (j + 1)
   std::map<std::pair<int, int>, BiquadTab*> kw_tabs;  // (M, chunk) -> device {hp, shelf}
   int rf_sizes = 1 << 14;   // resolution sizes on the register-FFT kernel (bit log2 N): the 16384-point one
@@ -351,8 +352,17 @@ struct omega_ctx {
   int* d_gcount[2] = {nullptr, nullptr};
   double* d_gsum[2] = {nullptr, nullptr};
   int HL = 0, HT = 0;
-  // staging for OMEGA_MEM_HOST
+  // staging for OMEGA_MEM_HOST: device slots, page-locked host slots for the inputs, and one device +
+  // page-locked output arena per call (every output of a call comes back in one D2H copy)
   std::vector<DevBuf> stage;
+  std::vector<DevBuf> pin;
+  DevBuf oarena, oarena_pin;
+  size_t oarena_used = 0, oarena_want = 0;
+  // the call's outputs may be written by the kernels straight into the page-locked arena (set by calls
+  // whose kernels only store their outputs: no output is read back by another workgroup)
+  bool zc_ok = false;
+  DevBuf zc_pin;
+  void* zc_dev = nullptr;
   std::vector<void*> allocs;
 };
 
@@ -364,7 +374,10 @@ int fail(omega_ctx* c, int code, const char* fmt, ...) {
   va_start(ap, fmt);
   std::vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
-  if (c) std::memcpy(c->err, buf, sizeof buf);
+  if (c) {
+    std::memcpy(c->err, buf, sizeof buf);
+    c->zc_ok = false;  // (a host call that fails before finish_host)
+  }
   return code;
 }
 
@@ -665,6 +678,23 @@ int build_spectral_tables(omega_ctx* c) {
     c->ent_end[r] = (int)all.size();
     c->ent_jmax[r] = 0;
     for (const CombEnt& en : er[r]) c->ent_jmax[r] = std::max(c->ent_jmax[r], en.j + 1);
+    // the magnitude pairs (k, K - k) holding every bin an entry reads (j and j + 1): one untangle per
+    // pair instead of two per entry, where that is fewer (ResParam::pair_lo / pair_hi)
+    const int K = cfg.res[r].fft_size / 2;
+    int plo = K, phi = -1;
+    for (const CombEnt& en : er[r]) {
+      if ((en.tm >> 24) == 2) continue;
+      for (int b = en.j; b <= en.j + 1; ++b) {
+        const int k = (b == K || b == K / 2) ? 0 : std::min(b, K - b);
+        plo = std::min(plo, k);
+        phi = std::max(phi, k);
+      }
+    }
+    c->pair_lo[r] = c->pair_hi[r] = 0;
+    if (phi >= 0 && K >= 2 && (phi + 1 - plo) < 2 * (int)er[r].size()) {
+      c->pair_lo[r] = plo;
+      c->pair_hi[r] = phi + 1;
+    }
   }
   std::vector<int> ooff(1, 0), orj;
   std::vector<float> ofr;
@@ -739,6 +769,8 @@ SpectralParams spectral_params(omega_ctx* c) {
     q.ent_end = c->ent_end[r];
     q.cw = (float)c->cfg.res[r].weight;
     q.low_band = c->ent_jmax[r] < 256;
+    q.pair_lo = c->pair_lo[r];
+    q.pair_hi = c->pair_hi[r];
   }
   p.ent = c->d_ent;
   p.T = c->cfg.target_bins;
@@ -754,27 +786,99 @@ struct HostOut {
   void* host;
   void* dev;
   size_t bytes;
+  size_t arena_off;  // offset in the output arena, or ~0 (a slot of its own)
 };
 
+// Page-locked host buffer of at least `bytes` (grown on demand; hipHostMalloc).
+int pinned_buf(omega_ctx* c, DevBuf& b, size_t bytes) {
+  if (b.n >= bytes) return 0;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.n = 0;
+  const size_t n = std::max<size_t>(bytes, 4096);
+  const hipError_t e = hipHostMalloc(&b.p, n, hipHostMallocDefault);
+  if (e != hipSuccess) return fail(c, OMEGA_ENOMEM, "staging hipHostMalloc(%zu): %s", n, hipGetErrorString(e));
+  b.n = n;
+  return 0;
+}
+
+// Host input -> device-visible buffer: copied into the slot's page-locked buffer on the CPU. Up to
+// kZeroCopyIn bytes the kernels read it there (one fabric read per element, no copy command before the
+// launch); larger inputs follow with an async H2D copy into the slot's device buffer (a pageable source
+// would make the runtime stage and wait on every copy).
+constexpr size_t kZeroCopyIn = 256 * 1024;
+constexpr size_t kZeroCopyOut = 256 * 1024;
+constexpr size_t kZeroCopyTag = (size_t)1 << 62;  // HostOut::arena_off of an output in zc_pin
 int stage_in(omega_ctx* c, int slot, const void* host, size_t bytes, const void** dev) {
-  void* d = nullptr;
-  int e = stage_buf(c, slot, bytes, &d);
+  if ((int)c->pin.size() <= slot) c->pin.resize(slot + 1);
+  int e = pinned_buf(c, c->pin[slot], bytes);
   if (e) return e;
-  HIPC(c, hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, c->stream));
+  if (bytes) std::memcpy(c->pin[slot].p, host, bytes);
+  if (bytes <= kZeroCopyIn) {
+    void* dp = nullptr;
+    HIPC(c, hipHostGetDevicePointer(&dp, c->pin[slot].p, 0));
+    *dev = dp;
+    return 0;
+  }
+  void* d = nullptr;
+  e = stage_buf(c, slot, bytes, &d);
+  if (e) return e;
+  HIPC(c, hipMemcpyAsync(d, c->pin[slot].p, bytes, hipMemcpyHostToDevice, c->stream));
   *dev = d;
   return 0;
 }
 
+// Host output: a device range of the call's output arena (outs empty: the call's first output resets
+// it; an arena too small for this call is grown at the next call, this call's outputs past it use their
+// own slots). finish_host copies the arena back in one D2H copy.
 template <class T>
 int stage_out(omega_ctx* c, int slot, T* host, size_t count, std::vector<HostOut>& outs, T** dev) {
   if (!host) {
     *dev = nullptr;
     return 0;
   }
+  const size_t bytes = count * sizeof(T);
+  if (c->zc_ok) {
+    // small outputs of a store-only call: straight into page-locked memory (no copy command after the
+    // kernels; finish_host only copies them to the caller's buffers on the CPU)
+    if (outs.empty()) c->oarena_used = 0;
+    const size_t off = (c->oarena_used + 255) & ~(size_t)255;
+    if (off + bytes <= kZeroCopyOut) {
+      if (!c->zc_pin.p) {
+        if (int e = pinned_buf(c, c->zc_pin, kZeroCopyOut)) return e;
+        HIPC(c, hipHostGetDevicePointer(&c->zc_dev, c->zc_pin.p, 0));
+      }
+      c->oarena_used = off + bytes;
+      outs.push_back({host, static_cast<char*>(c->zc_pin.p) + off, bytes, kZeroCopyTag + off});
+      *dev = reinterpret_cast<T*>(static_cast<char*>(c->zc_dev) + off);
+      return 0;
+    }
+  }
+  if (outs.empty()) {
+    c->oarena_used = 0;
+    if (c->oarena_want > c->oarena.n) {
+      const size_t n = c->oarena_want + c->oarena_want / 4;
+      if (c->oarena.p) (void)hipFree(c->oarena.p);
+      c->oarena.p = nullptr;
+      c->oarena.n = 0;
+      if (hipMalloc(&c->oarena.p, n) == hipSuccess) {
+        c->oarena.n = n;
+        if (int e = pinned_buf(c, c->oarena_pin, n)) return e;
+      }
+    }
+  }
+  const size_t off = (c->oarena_used + 255) & ~(size_t)255;
+  if (off + bytes <= c->oarena.n && c->oarena_pin.n >= c->oarena.n) {
+    c->oarena_used = off + bytes;
+    outs.push_back({host, static_cast<char*>(c->oarena.p) + off, bytes, off});
+    *dev = reinterpret_cast<T*>(static_cast<char*>(c->oarena.p) + off);
+    return 0;
+  }
+  c->oarena_want = std::max(c->oarena_want, off + bytes);
   void* d = nullptr;
-  int e = stage_buf(c, slot, count * sizeof(T), &d);
+  int e = stage_buf(c, slot, bytes, &d);
   if (e) return e;
-  outs.push_back({host, d, count * sizeof(T)});
+  outs.push_back({host, d, bytes, ~(size_t)0});
   *dev = static_cast<T*>(d);
   return 0;
 }
@@ -797,9 +901,23 @@ int check_device_err(omega_ctx* c) {
 // Host-memory calls: copy the outputs back and wait; an ordering wait of THIS call that expired is
 // reported by this call (device-memory calls report it at the next call or omega_synchronize).
 int finish_host(omega_ctx* c, const std::vector<HostOut>& outs) {
-  for (const HostOut& o : outs) HIPC(c, hipMemcpyAsync(o.host, o.dev, o.bytes, hipMemcpyDeviceToHost, c->stream));
+  c->zc_ok = false;
+  size_t span = 0;
+  for (const HostOut& o : outs) {
+    if (o.arena_off == ~(size_t)0)
+      HIPC(c, hipMemcpyAsync(o.host, o.dev, o.bytes, hipMemcpyDeviceToHost, c->stream));
+    else if (o.arena_off < kZeroCopyTag)
+      span = std::max(span, o.arena_off + o.bytes);
+  }
+  if (span) HIPC(c, hipMemcpyAsync(c->oarena_pin.p, c->oarena.p, span, hipMemcpyDeviceToHost, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
-  if (c->fork[0]) HIPC(c, hipStreamSynchronize(c->fork[0]));
+  if (c->fork[0] && hipStreamQuery(c->fork[0]) != hipSuccess) HIPC(c, hipStreamSynchronize(c->fork[0]));
+  for (const HostOut& o : outs) {
+    if (o.arena_off == ~(size_t)0) continue;
+    const char* src = o.arena_off >= kZeroCopyTag ? static_cast<const char*>(o.dev)
+                                                   : static_cast<char*>(c->oarena_pin.p) + o.arena_off;
+    std::memcpy(o.host, src, o.bytes);
+  }
   return check_device_err(c);
 }
 
@@ -994,6 +1112,17 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   // vs 64-65 us without meters)
   bp.q_begin = (int)body_end;
   bp.q_n = (int)q_n;
+#ifndef OMEGA_SEG_MID
+#define OMEGA_SEG_MID 1
+#endif
+  if (OMEGA_SEG_MID && fold && q_n > 0 && q_n % 8 == 0 && bp.seg_begin[1] > 0) {
+    // pipelined: the previous call's segment waits for nothing, so it goes between segment 0 and the
+    // true peaks instead of last, where its ~9 us latency-bound workgroups lengthened the tail (a
+    // multiple of 8 workgroups keeps every frame's roles on one XCD)
+    bp.q_begin = bp.seg_begin[1];
+    bp.seg_start[1] += (int)q_n;
+    bp.multi_start += (int)q_n;
+  }
   const int64_t grid = body_end + q_n;
   if (grid > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
   MeterPrepParams mq{};
@@ -1734,6 +1863,11 @@ void omega_destroy(omega_ctx* c) try {
     if (q) (void)hipFree(q);
   for (DevBuf& b : c->stage)
     if (b.p) (void)hipFree(b.p);
+  for (DevBuf& b : c->pin)
+    if (b.p) (void)hipHostFree(b.p);
+  if (c->oarena.p) (void)hipFree(c->oarena.p);
+  if (c->oarena_pin.p) (void)hipHostFree(c->oarena_pin.p);
+  if (c->zc_pin.p) (void)hipHostFree(c->zc_pin.p);
   drop_graphs(c);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->d_tail) (void)hipFree(c->d_tail);
@@ -1859,6 +1993,9 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
   const size_t span = (size_t)((n_frames - 1) * frame_stride + (C - 1) * channel_stride + W);
   int e = 0;
   if (mem == OMEGA_MEM_HOST) {
+    // without meters every kernel of the call only stores its outputs: small ones go straight to
+    // page-locked memory (the meter path's true peaks are re-read across workgroups: device staging)
+    c->zc_ok = !meters;
     e = stage_in(c, 0, x, span * sizeof(float), reinterpret_cast<const void**>(&dx));
     if (!e) e = stage_out(c, 1, comb, ncf * T, outs, &comb);
     if (!e) e = stage_out(c, 2, out->lufs_inst, ncf, outs, &lufs);

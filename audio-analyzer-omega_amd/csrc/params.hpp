@@ -26,6 +26,11 @@ struct ResParam {
   float cw;              // combine weight (config.weight)
   int low_band;          // the entries read only bins < 256 (the 16384-point register FFT then forms
                          // just the lowest and highest 256 frequencies: RegFFT::run_low)
+  // combine without a magnitude output, when the entries read more bins than half their count: the
+  // magnitudes of the pairs (k, K - k), pair_lo <= k < pair_hi, into the spectrum's slots first (one
+  // untangle per pair), then the entries from them (two LDS reads each). pair_hi == 0: every entry
+  // untangles the two bins it reads itself.
+  int pair_lo, pair_hi;
 };
 
 struct SpectralParams {

@@ -407,30 +407,42 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
   FFT::store_spectrum(v, buf, t);
   __syncthreads();
   OMEGA_STAMP(3);
-  float mg[16];
-  float mnyq = 0.f, mx = 0.f;
+  // Each untangle of the pair (k, K - k) gives both bins: thread t takes the pairs k = t + NTH q, q < 8
+  // (k < K/2) -- bins k in mg[q], K - k = K - t - NTH q in mgm[q] (t = 0, q = 0: bin 0 and the Nyquist
+  // bin K) -- and thread 0 the self-mirrored K/2 as well: half the untangles and half the mirror
+  // reads of one untangle per bin.
+  float mg[8], mgm[8];
+  float mx = 0.f, mhalf = 0.f;
   {
     const float2* bo = buf + FFT::s3(t);
     const float2* bm = buf + FFT::s3m(t);
-    static_for<0, 16>([&](auto q) {
+    static_for<0, 8>([&](auto q) {
       const float2 a = bo[FFT::o3(q)];
       const float2 b = bm[FFT::o3(15 - q)];
       float2 xk, xkk;
       untangle(a, b, twc<q, 32>(wm), xk, xkk);
       mg[q] = cabs(xk);
+      mgm[q] = cabs(xkk);
       if constexpr (q == 0) {
         if (t == 0) {
           mg[0] = fabsf(a.x + a.y);
-          mnyq = fabsf(a.x - a.y);
+          mgm[0] = fabsf(a.x - a.y);
         }
       }
-      mx = fmaxf(mx, mg[q]);
+      mx = fmaxf(mx, fmaxf(mg[q], mgm[q]));
     });
+    if (t == 0) {
+      mhalf = cabs(bo[FFT::o3(8)]);  // X[K/2] = conj(Z[K/2])
+      mx = fmaxf(mx, mhalf);
+    }
   }
-  mx = wave_max(fmaxf(mx, mnyq));
+  mx = wave_max(mx);
   __syncthreads();  // the untangle reads are done: the buffer becomes the magnitude array
-  static_for<0, 16>([&](auto q) { magc[t + NTH * q] = mg[q]; });
-  if (t == 0) magc[K] = mnyq;
+  static_for<0, 8>([&](auto q) {
+    magc[t + NTH * q] = mg[q];
+    magc[K - t - NTH * q] = mgm[q];
+  });
+  if (t == 0) magc[K / 2] = mhalf;
   if ((t & 63) == 0) redf[t >> 6] = mx;
   for (int i = t; i < kFlagWords; i += NTH) sflag[i] = 0u;
   OMEGA_STAMP(4);
@@ -451,8 +463,11 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
   OMEGA_STAMP(5);
   if (p.mag_out) {
     float* o = p.mag_out + fr * (K + 1);
-    static_for<0, 16>([&](auto q) { o[t + NTH * q] = mg[q]; });
-    if (t == 0) o[K] = mnyq;
+    static_for<0, 8>([&](auto q) {
+      o[t + NTH * q] = mg[q];
+      o[K - t - NTH * q] = mgm[q];
+    });
+    if (t == 0) o[K / 2] = mhalf;
   }
   if (p.bands_out) {
     float* o = p.bands_out + fr * p.n_out;

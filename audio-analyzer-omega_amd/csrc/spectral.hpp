@@ -29,12 +29,14 @@ __device__ __forceinline__ int magidx(int k) {
 
 // Magnitudes from the packed complex FFT in buf (BlockFFT<K> output order). Pair (k, K-k) is owned
 // by one thread, which overwrites only the imaginary slots of the two entries it read: no barrier
-// between reads and writes, nothing held in registers.
+// between reads and writes, nothing held in registers. Pairs k0 <= k < k1 (pair 0 carries bins 0, K
+// and K/2).
 template <int K, int NTH>
-__device__ __forceinline__ void rfft_magnitudes(float2* buf, const float2* __restrict__ twN, int tid) {
+__device__ __forceinline__ void rfft_magnitudes(float2* buf, const float2* __restrict__ twN, int tid, int k0 = 0,
+                                                int k1 = K / 2) {
   using FFT = BlockFFT<K, NTH>;
   float* mag = reinterpret_cast<float*>(buf);
-  for (int k = tid; k < K / 2; k += NTH) {
+  for (int k = k0 + tid; k < k1; k += NTH) {
     if (k == 0) {
       const float2 z = buf[FFT::out(0)];
       const float2 zm = buf[FFT::out(K / 2)];
@@ -69,7 +71,7 @@ __device__ __forceinline__ void mrfft_frame(const SpectralParams& p, int r, int6
   using FFT = BlockFFT<K, NTH>;
   OMEGA_STAMP(10 + 4 * (ilog2(K) - 9));
   const typename FFT::Tw tw = FFT::load_tw(p.tw[ilog2(K)], tid);
-  constexpr int EP = NTH >= 256 ? 1 : 256 / NTH;
+  constexpr int EP = NTH >= 256 ? 1 : (NTH >= 128 ? 256 / NTH : 512 / NTH);
   CombEnt ent[EP];
   static_for<0, EP>([&](auto i) {
     const int e = rp.ent_begin + tid + i * NTH;
@@ -81,7 +83,8 @@ __device__ __forceinline__ void mrfft_frame(const SpectralParams& p, int r, int6
     return make_float2(a.x * w.x, a.y * w.y);
   });
   OMEGA_STAMP(11 + 4 * (ilog2(K) - 9));
-  if (!rp.mag_out) {
+  const bool pair_range = !rp.mag_out && rp.pair_hi > 0;
+  if (!rp.mag_out && !pair_range) {
     // combine only (no magnitude output; uniform over the workgroup's groups): each entry untangles
     // the two bins it reads straight from the packed spectrum -- the combine reads a few hundred of
     // the K + 1 bins, so the all-bin magnitude pass and its barrier are skipped
@@ -115,7 +118,8 @@ __device__ __forceinline__ void mrfft_frame(const SpectralParams& p, int r, int6
     for (int e = rp.ent_begin + tid + EP * NTH; e < rp.ent_end; e += NTH) apply(p.ent[e]);
     return;
   }
-  rfft_magnitudes<K, NTH>(buf, p.tw[ilog2(2 * K)], tid);
+  // (combine only over many bins: just the pairs the entries read, ResParam::pair_lo / pair_hi)
+  rfft_magnitudes<K, NTH>(buf, p.tw[ilog2(2 * K)], tid, pair_range ? rp.pair_lo : 0, pair_range ? rp.pair_hi : K / 2);
   OMEGA_STAMP(12 + 4 * (ilog2(K) - 9));
   if (!valid) return;
   const float* mag = reinterpret_cast<const float*>(buf);

@@ -14,8 +14,11 @@ from dataclasses import dataclass
 from enum import Enum
 from typing import Dict, NamedTuple, Tuple
 
+import ctypes as C
+
 import numpy as np
 
+from . import _lib as L
 from .engine import Engine, Resolution
 
 logger = logging.getLogger(__name__)
@@ -88,17 +91,21 @@ class MultiResolutionFFT:
     # them again. Here they invalidate the device contexts built from configs.
     def _setup_windows(self):
         self._engines = {}
+        self._calls = {}
 
     def _setup_buffers(self):
         self._wmax = max(c.fft_size for c in self.configs)
-        self._ring = np.zeros(self._wmax, np.float32)
+        self._ring = np.zeros(max(512, self._wmax), np.float32)  # (the last _wmax samples at the end)
         self._written = 0
+        self._calls = {}
+        self._tfreqs = {}
 
     def _setup_frequency_arrays(self):
         self.freq_arrays = {i: np.fft.rfftfreq(c.fft_size, 1 / self.sample_rate) for i, c in enumerate(self.configs)}
 
     def _setup_working_arrays(self):
         self._engines = {}
+        self._calls = {}
 
     def _resolutions(self):
         return [Resolution(tuple(c.freq_range), c.fft_size, c.hop_size, c.weight, _win_name(c.window_type))
@@ -114,6 +121,27 @@ class MultiResolutionFFT:
             self._engines[key] = eng
         return eng
 
+    def _chunk_call(self, apply_weighting: bool, avail, full: bool):
+        """The per-chunk device call, prepared once per (configs, weighting, available resolutions): the
+        C ABI's output struct over persistent host arrays (the results get copies), so a call is one
+        ctypes call on the ring (host memory; omega_process_frames stages it page-locked and returns
+        every output in one copy)."""
+        key = (apply_weighting, tuple(avail), full, tuple((c.freq_range, c.fft_size, c.weight, c.window_type)
+                                                           for c in self.configs))
+        prep = self._calls.get(key)
+        if prep is None:
+            eng = self._engine(apply_weighting)
+            outs = L.Outputs()
+            mags = {i: np.empty((1, self.configs[i].fft_size // 2 + 1), np.float32) for i in avail}
+            for i, a in mags.items():
+                outs.mag[i] = a.ctypes.data
+            comb = np.empty((1, eng.T), np.float32) if full else None
+            if comb is not None:
+                outs.combined = comb.ctypes.data
+            prep = (eng, outs, mags, comb)
+            self._calls[key] = prep
+        return prep
+
     def process_audio_chunk(self, audio_chunk: np.ndarray, apply_weighting: bool = True) -> Dict[int, FFTResult]:
         """multi_resolution_fft.py:228-302."""
         if audio_chunk is None or len(audio_chunk) == 0:
@@ -124,22 +152,29 @@ class MultiResolutionFFT:
             if self._wmax != max(c.fft_size for c in self.configs):
                 self._setup_buffers()
             chunk = np.asarray(audio_chunk, dtype=np.float32).ravel()
-            if len(chunk) >= self._wmax:
-                self._ring[:] = chunk[-self._wmax:]
-            else:
-                self._ring = np.roll(self._ring, -len(chunk))
-                self._ring[-len(chunk):] = chunk
-            self._written = min(self._written + len(chunk), 1 << 62)
+            ring, n = self._ring, len(chunk)
+            if n >= self._wmax:
+                ring[-self._wmax:] = chunk[-self._wmax:]
+            else:  # (in place: the ring's address stays what the prepared calls hold)
+                ring[:-n] = ring[n:]
+                ring[-n:] = chunk
+            self._written = min(self._written + n, 1 << 62)
             avail = [i for i, c in enumerate(self.configs) if self._written >= c.fft_size]
             results: Dict[int, FFTResult] = {}
+            self._last = None
             if avail:
-                eng = self._engine(apply_weighting)
-                frame = self._ring if self._wmax >= 512 else np.concatenate([np.zeros(512 - self._wmax, np.float32), self._ring])
-                out = eng.process_frames(frame, 1, eng.W, eng.W, combined=False, lufs=False, true_peak=False,
-                                         mags=avail)
+                # with the weighted magnitudes of every resolution, the same launch also forms their
+                # combine (1024 targets, multi_resolution_fft.py:335-408): combine_results_optimized of
+                # exactly these results then needs no second device round trip
+                full = apply_weighting and len(avail) == len(self.configs)
+                eng, outs, mags, comb = self._chunk_call(apply_weighting, avail, full)
+                L.check(eng._ctx, L.lib().omega_process_frames(eng._ctx, ring.ctypes.data, 1, eng.W, eng.W,
+                                                                C.byref(outs), L.MEM_HOST))
                 for i in avail:
-                    results[i] = FFTResult(magnitude=out[f"mag{i}"][0].copy(), frequencies=self.freq_arrays[i],
+                    results[i] = FFTResult(magnitude=mags[i][0].copy(), frequencies=self.freq_arrays[i],
                                            config_index=i)
+                if full:
+                    self._last = ({i: (results[i].magnitude, mags[i][0]) for i in avail}, comb[0])
             self.processing_stats["total_calls"] += 1
             self.processing_stats["total_time"] += time.perf_counter() - start
             return results
@@ -166,6 +201,12 @@ class MultiResolutionFFT:
             logger.warning("No FFT results to combine")
             return np.zeros(target_bins), np.linspace(0, self.max_freq, target_bins)
         try:
+            last = getattr(self, "_last", None)
+            if last is not None and target_bins == 1024 and self._same_results(results, last[0]):
+                tf = self._tfreqs.get((self.max_freq, 1024))
+                if tf is None:
+                    tf = self._tfreqs[(self.max_freq, 1024)] = np.linspace(0, self.max_freq, 1024)
+                return last[1].copy(), tf.copy()
             target_freqs = np.linspace(0, self.max_freq, target_bins)
             eng = self._engine(True, target_bins)
             mags = {r.config_index: r.magnitude for r in results.values()}
@@ -175,11 +216,24 @@ class MultiResolutionFFT:
             logger.error(f"FFT result combination failed: {e}")
             return np.zeros(target_bins), np.linspace(0, self.max_freq, target_bins)
 
+    @staticmethod
+    def _same_results(results, ref) -> bool:
+        """results are the last process_audio_chunk's, unmodified: every resolution present with its own
+        magnitude array object holding the values the device returned."""
+        if len(results) != len(ref):
+            return False
+        for r in results.values():
+            got = ref.get(getattr(r, "config_index", None))
+            if got is None or r.magnitude is not got[0] or not np.array_equal(got[0], got[1]):
+                return False
+        return True
+
     def get_frequency_arrays(self) -> Dict[int, np.ndarray]:
         return self.freq_arrays.copy()
 
     def reset_all_buffers(self):
         self._ring.fill(0)
+        self._last = None
         self._written = 0
         logger.info("All buffers reset")
 

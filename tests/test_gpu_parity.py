@@ -85,6 +85,27 @@ def test_mrfft_golden_northstar(mr, k):
     assert normwise(c, mr[f"ns{k}/comb512"]) < SPEC_TOL
 
 
+def test_mrfft_combine_reuse_needs_unmodified_results(mr):
+    """process_audio_chunk forms the 1024-target combine in the same launch and combine_results_optimized
+    returns it only for exactly those results, unmodified: a magnitude changed in place, or a dict from
+    elsewhere, is combined on the device from the values given (as the reference combines whatever it
+    is handed)."""
+    m = _mrfft()
+    x = mr["triad_4096/x"]
+    res = m.process_audio_chunk(x)
+    c0, _ = m.combine_results_optimized(res, 1024)
+    assert normwise(c0, mr["triad_4096/comb1024"]) < SPEC_TOL
+    res[1].magnitude[:] *= 3.0
+    c1, _ = m.combine_results_optimized(res, 1024)
+    fresh = _mrfft()
+    c2, _ = fresh.combine_results_optimized(res, 1024)  # (no cached launch: the combine kernel)
+    np.testing.assert_array_equal(c1, c2)
+    assert normwise(c1, c0) > 1e-3
+    copied = {i: r._replace(magnitude=r.magnitude.copy()) for i, r in m.process_audio_chunk(x).items()}
+    c3, _ = m.combine_results_optimized(copied, 1024)
+    np.testing.assert_array_equal(c3, fresh.combine_results_optimized(copied, 1024)[0])
+
+
 SMALL = [((20, 2000), 256, 128, 1.5), ((200, 6000), 128, 64, 1.2), ((1000, 12000), 64, 32, 1.0),
          ((5000, 20000), 512, 256, 1.5)]
 
