@@ -11,6 +11,10 @@
 //   mul-2bank   v_mul_f32 vN, vN, v(80 + (N+1)%4)
 //   pkfma       v_pk_fma_f32 on 8 register pairs (v64..v79), constants v[80:81], v[82:83]
 //   fma-3b-x8   fma-3bank with 128 instructions per loop iteration (one branch per 128)
+//   pkadd-cf    v_pk_add_f32, the two 64-bit sources in distinct bank pairs (banks 0-1 / 2-3)
+//   pkadd-cfl   v_pk_add_f32, both sources in the same bank pair
+//   pkmul-cf    v_pk_mul_f32, distinct bank pairs
+//   pkfma-s12   v_pk_fma_f32 with src1 = src2 (one register pair), distinct from src0's bank pair
 // Every workgroup reads s_memtime (shader cycles) at entry and exit, so cycles per wave-instruction per
 // SIMD = workgroup cycles / (resident waves per SIMD x instructions per wave), with every workgroup
 // resident at once (grid = 256 CUs x workgroups per CU, LDS sized to hold that occupancy).
@@ -49,6 +53,18 @@
   A2(op, 78, 83) A2(op, 79, 80)
 #define PK(n, m) "v_pk_fma_f32 v[" #n ":" #m "], v[" #n ":" #m "], v[80:81], v[82:83]\n"
 #define BODY_PK PK(64, 65) PK(66, 67) PK(68, 69) PK(70, 71) PK(72, 73) PK(74, 75) PK(76, 77) PK(78, 79)
+// packed ops with the 64-bit operands in distinct bank pairs (v[4i:4i+1] banks 0-1, v[4i+2:4i+3] 2-3)
+#define P2(op, n, m, a, b) op " v[" #n ":" #m "], v[" #n ":" #m "], v[" #a ":" #b "]\n"
+#define BODY_P2CF(op)                                                                                          \
+  P2(op, 64, 65, 82, 83) P2(op, 66, 67, 80, 81) P2(op, 68, 69, 82, 83) P2(op, 70, 71, 80, 81)                  \
+  P2(op, 72, 73, 82, 83) P2(op, 74, 75, 80, 81) P2(op, 76, 77, 82, 83) P2(op, 78, 79, 80, 81)
+#define BODY_P2CL(op)                                                                                          \
+  P2(op, 64, 65, 80, 81) P2(op, 66, 67, 82, 83) P2(op, 68, 69, 80, 81) P2(op, 70, 71, 82, 83)                  \
+  P2(op, 72, 73, 80, 81) P2(op, 74, 75, 82, 83) P2(op, 76, 77, 80, 81) P2(op, 78, 79, 82, 83)
+#define P3(n, m, a, b) "v_pk_fma_f32 v[" #n ":" #m "], v[" #n ":" #m "], v[" #a ":" #b "], v[" #a ":" #b "]\n"
+#define BODY_PFS                                                                                               \
+  P3(64, 65, 82, 83) P3(66, 67, 80, 81) P3(68, 69, 82, 83) P3(70, 71, 80, 81) P3(72, 73, 82, 83)               \
+  P3(74, 75, 80, 81) P3(76, 77, 82, 83) P3(78, 79, 80, 81)
 
 template <int OP>
 __global__ __launch_bounds__(1024) void issue_kernel(float* out, unsigned long long* tim, int iters) {
@@ -70,6 +86,10 @@ __global__ __launch_bounds__(1024) void issue_kernel(float* out, unsigned long l
     if constexpr (OP == 4) asm volatile(BODY_2("v_add_f32") ::: CLOB);
     if constexpr (OP == 5) asm volatile(BODY_2("v_mul_f32") ::: CLOB);
     if constexpr (OP == 6) asm volatile(BODY_PK ::: CLOB);
+    if constexpr (OP == 8) asm volatile(BODY_P2CF("v_pk_add_f32") ::: CLOB);
+    if constexpr (OP == 9) asm volatile(BODY_P2CL("v_pk_add_f32") ::: CLOB);
+    if constexpr (OP == 10) asm volatile(BODY_P2CF("v_pk_mul_f32") ::: CLOB);
+    if constexpr (OP == 11) asm volatile(BODY_PFS ::: CLOB);
     if constexpr (OP == 7) asm volatile(BODY_FMA3 BODY_FMA3 BODY_FMA3 BODY_FMA3 BODY_FMA3 BODY_FMA3 BODY_FMA3 BODY_FMA3 ::: CLOB);
   }
   const unsigned long long c1 = __builtin_amdgcn_s_memtime();
@@ -110,7 +130,7 @@ void run(const char* name, int threads, int wg_per_cu, int iters, float* d, unsi
   }
   std::sort(cyc.begin(), cyc.end());
   const double per_simd = (double)wg_per_cu * threads / 64 / 4;  // resident waves per SIMD
-  const int ipw = OP == 6 ? 8 : (OP == 7 ? 128 : 16);                                // instructions per iteration
+  const int ipw = (OP == 6 || OP >= 8) ? 8 : (OP == 7 ? 128 : 16);                                // instructions per iteration
   const double inst = per_simd * iters * ipw;
   printf("%-11s waves/SIMD %4.1f  cycles per wave-instr per SIMD: p50 %.3f  max %.3f   (kernel %.3f ms)\n", name,
          per_simd, cyc[cyc.size() / 2] / inst, cyc.back() / inst, ms_best);
@@ -135,6 +155,10 @@ int main() {
     run<5>("mul-2bank", o.threads, o.wg, it, d, t);
     run<6>("pkfma", o.threads, o.wg, it, d, t);
     run<7>("fma-3b-x8", o.threads, o.wg, it / 8, d, t);
+    run<8>("pkadd-cf", o.threads, o.wg, it, d, t);
+    run<9>("pkadd-cfl", o.threads, o.wg, it, d, t);
+    run<10>("pkmul-cf", o.threads, o.wg, it, d, t);
+    run<11>("pkfma-s12", o.threads, o.wg, it, d, t);
   }
   return 0;
 }

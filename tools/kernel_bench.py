@@ -65,11 +65,23 @@ def main():
     outs = L.Outputs()
     outs.combined, outs.lufs_inst, outs.true_peak_db = comb.data_ptr(), out["li"].data_ptr(), out["tp"].data_ptr()
 
+    # the batch kernel without one role (its marginal cost inside the mixed grid)
+    part = {}
+    for nm, drop in (("batch-nores", "combined"), ("batch-notp", "true_peak_db"), ("batch-nokw", "lufs_inst")):
+        o2 = L.Outputs()
+        o2.combined, o2.lufs_inst, o2.true_peak_db = outs.combined, outs.lufs_inst, outs.true_peak_db
+        setattr(o2, drop, None)
+        part[nm] = o2
+
     def run():
         if a.stage == "batch":  # one batch_kernel launch: the step's per-channel-frame work, no meters
             import ctypes
             eng._check(lib.omega_process_frames(eng._ctx, x.data_ptr(), F, 2 * 16384, 16384, ctypes.byref(outs),
                                                 L.MEM_DEVICE))
+        if a.stage in part:
+            import ctypes
+            eng._check(lib.omega_process_frames(eng._ctx, x.data_ptr(), F, 2 * 16384, 16384,
+                                                ctypes.byref(part[a.stage]), L.MEM_DEVICE))
         if a.stage == "spectra":
             e3.spectra(x3, "hann", bands=bt, chroma=True, out=so)
         if a.stage == "drums":

@@ -35,8 +35,10 @@ print(f"{sys.argv[3]}: window {w[1]-w[0] if w else 0:.1f} s; power W n {len(p)} 
 PY
 }
 rocm-smi --showmaxpower 2>/dev/null | grep -i "power" | head -2 | tee "$OUT" || true
-spid=$(sample gpurun_out/smi_batch_cont.txt)
-timeout -k 10 150 python tools/kernel_bench.py batch --frames 4096 --reps ${REPS:-9000} > gpurun_out/power_batch_bench.log 2>&1
-kill $spid 2>/dev/null || true; wait $spid 2>/dev/null || true
-tail -1 gpurun_out/power_batch_bench.log | tee -a "$OUT"
-summ gpurun_out/smi_batch_cont.txt gpurun_out/power_batch_bench.log batch | tee -a "$OUT"
+for st in ${STAGES:-batch}; do
+  spid=$(sample gpurun_out/smi_${st}_cont.txt)
+  timeout -k 10 150 python tools/kernel_bench.py $st --frames 4096 --reps ${REPS:-9000} > gpurun_out/power_${st}_bench.log 2>&1
+  kill $spid 2>/dev/null || true; wait $spid 2>/dev/null || true
+  tail -1 gpurun_out/power_${st}_bench.log | tee -a "$OUT"
+  summ gpurun_out/smi_${st}_cont.txt gpurun_out/power_${st}_bench.log $st | tee -a "$OUT"
+done

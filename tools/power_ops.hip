@@ -59,8 +59,9 @@ constexpr int kLds = 72 * 1024;
 
 #define PK(n, m) "v_pk_fma_f32 v[" #n ":" #m "], v[" #n ":" #m "], v[80:81], v[82:83]\n"
 #define BODY_PK PK(64, 65) PK(66, 67) PK(68, 69) PK(70, 71) PK(72, 73) PK(74, 75) PK(76, 77) PK(78, 79)
-#define PA(n, m) "v_pk_add_f32 v[" #n ":" #m "], v[" #n ":" #m "], v[80:81]\n"
-#define BODY_PA PA(64, 65) PA(66, 67) PA(68, 69) PA(70, 71) PA(72, 73) PA(74, 75) PA(76, 77) PA(78, 79)
+// (sources in distinct bank pairs: v[4i:4i+1] is banks 0-1, v[4i+2:4i+3] banks 2-3)
+#define PA(n, m, a, b) "v_pk_add_f32 v[" #n ":" #m "], v[" #n ":" #m "], v[" #a ":" #b "]\n"
+#define BODY_PA PA(64, 65, 82, 83) PA(66, 67, 80, 81) PA(68, 69, 82, 83) PA(70, 71, 80, 81) PA(72, 73, 82, 83) PA(74, 75, 80, 81) PA(76, 77, 82, 83) PA(78, 79, 80, 81)
 
 template <int OP>
 __global__ __launch_bounds__(kThreads, 4) void op_kernel(float* out, int iters) {
