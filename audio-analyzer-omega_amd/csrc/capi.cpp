@@ -40,6 +40,7 @@ hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s);
 hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_query(const MeterPrepParams& p, hipStream_t s);
+hipError_t launch_meter_load(const MeterLoadParams& p, hipStream_t s);
 hipError_t launch_bands(const BandParams& p, hipStream_t s);
 hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int hi, const double* mat, double* out,
                          hipStream_t s);
@@ -2414,6 +2415,38 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
   HIPC(c, hipEventRecord(c->ev_fork, c->stream));
   HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  return 0;
+} catch (...) {
+  return guard_fail(c);
+}
+
+int omega_meter_load_history(omega_ctx* c, const float* lufs_inst, int64_t n_l, const float* tp_db, int64_t n_t,
+                             int mem) try {
+  if (!c) return OMEGA_EINVAL;
+  if (n_l < 0 || n_t < 0 || n_t > n_l) return fail(c, OMEGA_EINVAL, "need 0 <= n_t <= n_l");
+  if (n_l > c->HL) return fail(c, OMEGA_EINVAL, "%lld LUFS rows exceed the %d-frame history", (long long)n_l, c->HL);
+  if ((n_l && !lufs_inst) || (n_t && !tp_db)) return fail(c, OMEGA_EINVAL, "null history");
+  if (int e = check_device_err(c)) return e;
+  HIPC(c, hipSetDevice(c->device));
+  if (int e = flush_meters(c)) return e;  // (a pending segment reads the state being replaced)
+  const int C = c->cfg.n_channels;
+  const float* dl = lufs_inst;
+  const float* dt = tp_db;
+  if (mem == OMEGA_MEM_HOST) {
+    int e = stage_in(c, 2, lufs_inst, (size_t)n_l * C * sizeof(float), reinterpret_cast<const void**>(&dl));
+    if (!e) e = stage_in(c, 3, tp_db, (size_t)n_t * C * sizeof(float), reinterpret_cast<const void**>(&dt));
+    if (e) return e;
+  }
+  // as omega_meter_update: after the side stream's last writes of the state, and before its next reads
+  HIPC(c, hipEventRecord(c->ev_join[1], c->fork[0]));
+  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[1], 0));
+  const int a = c->cur;
+  MeterLoadParams p{dl, dt, (int)n_l, (int)n_t, C, c->HL, c->HT, (float)c->cfg.gate_lufs, c->d_hist_l[a],
+                    c->d_hist_t[a], c->d_nl[a], c->d_nt[a], c->d_skeys[a], c->d_ns[a], c->d_t0[a]};
+  HIPC(c, launch_meter_load(p, c->stream));
+  HIPC(c, hipEventRecord(c->ev_fork, c->stream));
+  HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
+  if (mem == OMEGA_MEM_HOST) HIPC(c, hipStreamSynchronize(c->stream));
   return 0;
 } catch (...) {
   return guard_fail(c);

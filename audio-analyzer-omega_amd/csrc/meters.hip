@@ -100,6 +100,68 @@ __global__ __launch_bounds__(256) void meter_query_kernel(MeterPrepParams p) {
   }
 }
 
+// One 1024-thread workgroup per channel: the histories copied, the gated keys of the LUFS history
+// (order-preserving value key << 32 | absolute frame index, as meter_prep.hpp forms them) sorted by a
+// bitonic network over kMeterHistCap LDS slots (empty slots ~0: they sort last), the counts.
+__global__ __launch_bounds__(1024) void meter_load_kernel(MeterLoadParams p) {
+  __shared__ unsigned long long key[kMeterHistCap];
+  __shared__ int cnt;
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int C = p.C, nl = p.n_l;
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  int mine = 0;
+  for (int i = tid; i < kMeterHistCap; i += 1024) {
+    unsigned long long k = ~0ull;
+    if (i < nl) {
+      const float v = p.lufs[(int64_t)i * C + c];
+      p.hist_l[(int64_t)c * p.HL + i] = v;
+      if (v > p.gate) {
+        k = ((unsigned long long)fkey(v) << 32) | (unsigned long long)(uint32_t)i;
+        ++mine;
+      }
+    }
+    key[i] = k;
+  }
+  // the true-peak history: the last min(HT, n_l) frames; frames before the n_t given ones -100
+  const int kt = min(p.HT, nl);
+  for (int i = tid; i < kt; i += 1024) {
+    const int row = nl - kt + i, first = nl - p.n_t;
+    p.hist_t[(int64_t)c * p.HT + i] = row >= first ? p.tp[(int64_t)(row - first) * C + c] : -100.0f;
+  }
+  if (mine) atomicAdd(&cnt, mine);
+  __syncthreads();
+  for (int k = 2; k <= kMeterHistCap; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < kMeterHistCap; i += 1024) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = key[i], b = key[l];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            key[i] = b;
+            key[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int ns = cnt;
+  for (int i = tid; i < ns; i += 1024) p.skeys[(int64_t)c * p.HL + i] = key[i];
+  if (tid == 0) {
+    p.n_l_out[c] = nl;
+    p.n_t_out[c] = kt;
+    p.n_s_out[c] = ns;
+    p.t0_out[c] = (uint32_t)nl;
+  }
+}
+
+hipError_t launch_meter_load(const MeterLoadParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(meter_load_kernel, dim3((unsigned)p.C), dim3(1024), 0, s, p);
+  return hipGetLastError();
+}
+
 OMEGA_STAMPS_GETTER(omega_debug_meter_stamps)
 OMEGA_MARKS_GETTER(omega_debug_marks_meters)
 

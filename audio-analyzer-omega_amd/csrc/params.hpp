@@ -114,6 +114,24 @@ struct alignas(16) MeterExt {
   int pad;
 };
 
+// omega_meter_load_history: the meter state (parity cur) of a stream whose last n_l frames had the
+// LUFS_inst values lufs[f * C + c] and whose last n_t of them the true peaks tp[f * C + c] (time order),
+// the next frame at absolute index n_l -- what omega_meter_reset + omega_meter_update over those frames
+// leave (true peaks of the older frames -100), without computing their aggregates.
+struct MeterLoadParams {
+  const float* lufs;  // [n_l, C]
+  const float* tp;    // [n_t, C]
+  int n_l, n_t, C, HL, HT;
+  float gate;
+  float* hist_l;      // [C, HL]
+  float* hist_t;      // [C, HT]
+  int* n_l_out;
+  int* n_t_out;
+  unsigned long long* skeys;  // [C, HL]
+  int* n_s_out;
+  uint32_t* t0_out;
+};
+
 struct MeterPrepParams {
   const float* lufs;    // [n_frames * C] batch instantaneous LUFS
   const float* tp;      // [n_frames * C]

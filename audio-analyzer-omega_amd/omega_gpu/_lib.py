@@ -103,6 +103,7 @@ EXPORTS = {
                                   C.c_void_p, C.c_int]),
     "omega_meter_update": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]),
     "omega_meter_reset": (C.c_int, [C.c_void_p]),
+    "omega_meter_load_history": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int]),
     "omega_calculate_lufs": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_int32,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "omega_bands_create": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,

@@ -169,10 +169,17 @@ class TimeShardExchange:
 
 def meter_time_shard(engine, li: torch.Tensor, tp: torch.Tensor, hist: Tuple[torch.Tensor, torch.Tensor]):
     """Step (3)-(4) on one rank: load the exchanged history into the engine's meter state, then meter
-    the shard. `engine` offers reset_meters() and meter_update(li, tp, n_frames) over [n, C] rows
-    (omega_gpu.Engine on the device). Returns the shard's meters [n * C, 5]."""
-    engine.reset_meters()
-    hl, ht = history_frames(*hist)
-    if hl.shape[0]:
-        engine.meter_update(hl.contiguous(), ht.contiguous(), hl.shape[0])
+    the shard. `engine` offers load_meter_history(li, tp) (omega_gpu.Engine: omega_meter_load_history,
+    one kernel writing the state) or else reset_meters() + meter_update(li, tp, n_frames) over [n, C]
+    rows (the history replayed as pseudo-frames; the CPU stand-in of the tests). Returns the shard's
+    meters [n * C, 5]."""
+    hl, ht = hist
+    if hasattr(engine, "load_meter_history"):
+        k = min(ht.shape[0], hl.shape[0])
+        engine.load_meter_history(hl.contiguous(), ht[ht.shape[0] - k:].contiguous())
+    else:
+        engine.reset_meters()
+        hl, ht = history_frames(*hist)
+        if hl.shape[0]:
+            engine.meter_update(hl.contiguous(), ht.contiguous(), hl.shape[0])
     return engine.meter_update(li.contiguous(), tp.contiguous(), li.shape[0])

@@ -243,6 +243,29 @@ class Engine:
                                               w.ctypes.data if w is not None else None, li.ctypes.data, L.MEM_HOST))
         return w, li
 
+    def load_meter_history(self, lufs_inst, tp_db):
+        """omega_meter_load_history: the meter state after a stream whose last frames had the LUFS_inst
+        rows lufs_inst [n_l, C] and, for the last n_t of them, the true-peak rows tp_db [n_t, C]
+        (time order; device torch float32 tensors or host numpy)."""
+        if _is_torch(lufs_inst):
+            import torch
+            li, tp = lufs_inst.contiguous(), tp_db.contiguous()
+            if li.dtype != torch.float32 or tp.dtype != torch.float32:
+                raise ValueError("load_meter_history: float32 rows")
+            if li.numel():
+                self._bind_stream(li)
+            mem = L.MEM_DEVICE
+        else:
+            li = np.ascontiguousarray(lufs_inst, dtype=np.float32)
+            tp = np.ascontiguousarray(tp_db, dtype=np.float32)
+            mem = L.MEM_HOST
+        n_l, n_t = li.shape[0] if li.ndim else 0, tp.shape[0] if tp.ndim else 0
+        if li.ndim != 2 or li.shape[1] != self.C or (n_t and (tp.ndim != 2 or tp.shape[1] != self.C)):
+            raise ValueError(f"load_meter_history: [n, {self.C}] rows")
+        self._check(L.lib().omega_meter_load_history(self._ctx, _ptr(li) if n_l else None, int(n_l),
+                                                     _ptr(tp) if n_t else None, int(n_t), mem))
+        self._held = None  # (the load ran a pending meter segment first)
+
     def meter_update(self, lufs_inst, tp_db, n_frames: int):
         """The A9 aggregates of n_frames x C injected (LUFS_inst, true peak) values in frame order
         (host numpy, or device torch float32 tensors: then the result is a device tensor too)."""

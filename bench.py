@@ -57,6 +57,7 @@ def parse(argv=None):
     ap.add_argument("--no-cfg3", action="store_true", help="skip the cfg3 / drums / app_post lines")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the cfg4 per-GPU-shard line")
     ap.add_argument("--cfg4-steps", type=int, default=20)
+    ap.add_argument("--no-rotating", action="store_true", help="skip the rotating-input variant of the headline")
     ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 sustained-stream line")
     ap.add_argument("--cfg5-seconds", type=float, default=60.0)
     # test hooks (tests/test_bench_launch.py): a stand-in compute backend on the CPU over gloo, a
@@ -188,6 +189,8 @@ def measure(be, rank, world, frames, steps, warmup, gather, seed_base=None, prep
     seconds, rank 0's last gathered blocks or None, layout)."""
     from omega_gpu import dist as D
     x, lay, bufs, recv = prep if prep is not None else prepare(be, rank, world, frames, seed_base)
+    # x: one resident batch, or a list of distinct batches rotated per step (the cache-cold variant)
+    xs = x if isinstance(x, (list, tuple)) else [x]
     views = [lay.views(b) for b in bufs]
     pending = [None, None]
     be.reset()
@@ -199,7 +202,7 @@ def measure(be, rank, world, frames, steps, warmup, gather, seed_base=None, prep
         if pending[b] is not None:
             pending[b].wait()
             pending[b] = None
-        be.process(x, frames, views[b])
+        be.process(xs[i % len(xs)], frames, views[b])
         j = i - lag
         if gather and j >= first:
             pending[j % 2] = D.gather_to_root(bufs[j % 2], recv[j % 2], async_op=True)
@@ -693,6 +696,20 @@ def main(argv=None):
     if a.dump and rank == 0 and got is not None:
         np.save(a.dump, torch.stack([g.cpu() for g in got]).numpy())
 
+    rotating = None
+    if not standin and not a.no_rotating:
+        # the same step over 8 distinct input batches rotated per step (8 x 33.5 MB = 268 MB, past the
+        # 256 MiB Infinity Cache): the headline reads one resident batch, whose second read by the
+        # true-peak role is an Infinity-Cache hit either way; this line shows what cold input costs
+        x0 = prep_main[0]
+        xr = [x0] + [x0 * (1.0 + 0.0625 * k) for k in range(1, 8)]
+        dtr, _, _ = measure(be, rank, world, frames, a.steps, a.warmup, gather,
+                            prep=(xr,) + tuple(prep_main[1:]))
+        rotating = {"workload": f"cfg2 step over 8 distinct resident input batches rotated per step "
+                                f"({8 * frames * C * W * 4 / 2**20:.0f} MiB > the 256 MiB Infinity Cache)",
+                    "value": frames * C * world * a.steps / dtr, "unit": "channel-frames/s",
+                    "ms_per_step": dtr / a.steps * 1e3}
+        del xr
     roof = None
     if not standin:
         # (right after the headline, on its input: no idle in between, see above)
@@ -742,6 +759,8 @@ def main(argv=None):
             line["backend"] = f"stand-in {a.standin} (CPU, {be.dist_backend}); not a measurement"
         if cfg4 is not None:
             line["cfg4"] = cfg4
+        if rotating is not None:
+            line["cfg2_rotating_inputs"] = rotating
         if cfg5 is not None:
             line["cfg5"] = cfg5
         if world == 1 and not a.no_cfg3 and not standin:

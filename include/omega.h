@@ -214,6 +214,15 @@ int omega_weighting(omega_ctx* ctx, const float* x, int64_t n, int32_t m, int32_
 int omega_meter_update(omega_ctx* ctx, const float* lufs_inst, const float* tp_db, int64_t n_frames,
                        double* meters, int mem);
 int omega_meter_reset(omega_ctx* ctx);
+/* The meter state of a stream whose last n_l frames had the instantaneous LUFS lufs_inst [n_l, C] and
+ * whose last n_t of them (n_t <= n_l) the true peaks tp_db [n_t, C] (time order, frame-major), the next
+ * frame following them: what omega_meter_reset + omega_meter_update over those n_l frames (the true
+ * peaks of the n_l - n_t older ones -100 dBTP) leave, written by one kernel without computing their
+ * aggregates (a time-sharded stream's rank loads the history before its shard; SURVEY §8(e),
+ * omega_gpu/dist.py meter_time_shard). n_l <= integrated_len - 1. Replaces the reference's deques
+ * (professional_meters.py:20-25) filled by calculate_lufs calls. */
+int omega_meter_load_history(omega_ctx* ctx, const float* lufs_inst, int64_t n_l, const float* tp_db, int64_t n_t,
+                             int mem);
 
 /* ProfessionalMetering.calculate_lufs (professional_meters.py:231-281) in one call: weighting `mode`
  * (LUFS_inst only, as omega_weighting), calculate_true_peak(x, oversampling) (as omega_true_peak_os)

@@ -711,6 +711,32 @@ def test_time_sharded_stream_meters_on_device():
         prev = D.stream_history(prev[0], prev[1], tails, world)
 
 
+@pytest.mark.parametrize("n_l,n_t", [(0, 0), (1, 1), (40, 40), (100, 30), (3599, 59), (2500, 0)])
+def test_meter_load_history_equals_replay(n_l, n_t):
+    """omega_meter_load_history writes the meter state of a stream with the given LUFS_inst / true-peak
+    history in one kernel; the shard metered after it is bitwise what the replay (reset, the history
+    through omega_meter_update as pseudo-frames with -100 true peaks before the given ones) gives --
+    gated and ungated values, a history shorter than the peak window, longer than the chunk."""
+    import torch
+    from omega_gpu import Engine, Resolution
+    from omega_gpu import dist as D
+    rng = np.random.default_rng(n_l + 7 * n_t)
+    hl = torch.from_numpy(rng.uniform(-90, -5, (n_l, 2)).astype(np.float32)).cuda()
+    ht = torch.from_numpy(rng.uniform(-40, 0, (n_t, 2)).astype(np.float32)).cuda()
+    sl = torch.from_numpy(rng.uniform(-80, -5, (300, 2)).astype(np.float32)).cuda()
+    st = torch.from_numpy(rng.uniform(-40, 0, (300, 2)).astype(np.float32)).cuda()
+    kw = dict(sample_rate=FS, max_freq=20000, target_bins=2, frame_size=512, n_channels=2)
+    a, b = (Engine([Resolution((20, 20000), 512, 256, 1.0)], **kw) for _ in range(2))
+    a.load_meter_history(hl, ht)
+    got = a.meter_update(sl, st, 300)
+    b.reset_meters()
+    rl, rt = D.history_frames(hl, ht)
+    if n_l:
+        b.meter_update(rl.contiguous(), rt.contiguous(), n_l)
+    ref = b.meter_update(sl, st, 300)
+    assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("pipe", [False, True])
 def test_many_contexts_default_layout(pipe):
     """The default layout's precondition (omega.h, omega_set_stream): the batch kernel and the meter
