@@ -1063,6 +1063,9 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   };
   // (measured: the true peaks in segment 0 beside the K-weighting, the 16384-point resolution in
   // segment 1, with or without the small resolutions before it: step 73.5-75.1 vs 68.8-70.5 us)
+  // (measured, round 5, pipelined step on one box: the K-weighting beside the true peaks with the
+  // 16384-point resolution after them, or the true peaks beside the 16384-point resolution with the
+  // K-weighting after them, 65.3-67.3 us against 65.3-67.1 for this order: the same)
   add(0, 0, do_kw);        // segment 0: K-weighting and the 16384-point resolution, groups of 8 frames
   add(0, 2, mr >= 0);
   add(1, 1, do_tp);        // segment 1: the true peaks
@@ -1113,17 +1116,8 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   // vs 64-65 us without meters)
   bp.q_begin = (int)body_end;
   bp.q_n = (int)q_n;
-#ifndef OMEGA_SEG_MID
-#define OMEGA_SEG_MID 1
-#endif
-  if (OMEGA_SEG_MID && fold && q_n > 0 && q_n % 8 == 0 && bp.seg_begin[1] > 0) {
-    // pipelined: the previous call's segment waits for nothing, so it goes between segment 0 and the
-    // true peaks instead of last, where its ~9 us latency-bound workgroups lengthened the tail (a
-    // multiple of 8 workgroups keeps every frame's roles on one XCD)
-    bp.q_begin = bp.seg_begin[1];
-    bp.seg_start[1] += (int)q_n;
-    bp.multi_start += (int)q_n;
-  }
+  // (measured, round 5: the pipelined segment between segment 0 and the true peaks instead, step
+  // 65.3-67.1 vs 66.5-66.6 us on one box: no difference)
   const int64_t grid = body_end + q_n;
   if (grid > 0x7FFFFFFF) return fail(c, OMEGA_EINVAL, "batch of %lld channel-frames too large", (long long)n);
   MeterPrepParams mq{};

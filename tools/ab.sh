@@ -28,7 +28,7 @@ fi
 run() {  # label, stage, lib args...
   local lab=$1 st=$2; shift 2
   if [ "$st" = step ]; then
-    echo "$lab step    $(timeout -k 10 120 python tools/step_probe.py --modes 0 --steps 400 "$@" | tail -1)"
+    echo "$lab step    $(timeout -k 10 120 python tools/step_probe.py --modes 0 --steps 400 ${PIPE:+--pipe} "$@" | tail -1)"
   else
     echo "$lab $st $(timeout -k 10 120 python tools/kernel_bench.py "$st" --reps 400 "$@" 2>/dev/null | tail -1)"
   fi
