@@ -281,6 +281,7 @@ struct omega_ctx {
   int rf_sizes = 1 << 14;   // resolution sizes on the register-FFT kernel (bit log2 N): the 16384-point one
   std::map<std::pair<int, int>, float*> windows;  // (m, kind) -> device window
   std::map<int, float2*> rots;                     // m -> true-peak rotation table
+  std::map<std::pair<int, int>, float4*> wgens;     // (m, kind) -> WinGen table
   // combine plan as per-target owner lists (CSR) for omega_combine over a subset of resolutions
   int* d_own_off = nullptr;
   int* d_own_rj = nullptr;  // (r << 24) | j
@@ -296,7 +297,7 @@ struct omega_ctx {
     float* w1 = nullptr;
     unsigned short* perm = nullptr;
     int* goff = nullptr;
-    float4* rec = nullptr;
+    float* rec = nullptr;
   } ctab;
   int n_cu = 0;
   // drum-feature stream state (omega_drum_features), double-buffered, for drum_bins bins per frame
@@ -503,6 +504,51 @@ int get_window(omega_ctx* c, int m, int kind, float** out) {
   int r = upload(c, &d, make_window(m, kind));
   if (r) return r;
   c->windows[key] = d;
+  *out = d;
+  return 0;
+}
+
+// The window of make_window as the register-FFT bodies' generator (regfft.hpp WinGen): with
+// phi = pi n / (M - 1), n = 1 - M + 2i, cos(phi) = -C_i and cos(2 phi) = 2 C_i^2 - 1, C_i = cos(2 pi i / (M - 1)),
+// so a0 + a1 cos(phi) + a2 cos(2 phi) = (a0 - a2) + C_i (-a1 + 2 a2 C_i); thread t of NTH = M / 32 takes the
+// points 2 (t + NTH q) + e
+int get_wingen(omega_ctx* c, int m, int kind, float4** out) {
+  auto key = std::make_pair(m, kind);
+  auto it = c->wgens.find(key);
+  if (it != c->wgens.end()) {
+    *out = it->second;
+    return 0;
+  }
+  if (m < 1024 || m % 32) return fail(c, OMEGA_EINVAL, "window generator: %d points", m);
+  double a0 = 1.0, a1 = 0.0, a2 = 0.0;
+  switch (kind) {
+    case OMEGA_WIN_BLACKMAN: a0 = 0.42; a1 = 0.5; a2 = 0.08; break;
+    case OMEGA_WIN_HANN: a0 = 0.5; a1 = 0.5; break;
+    case OMEGA_WIN_HAMMING: a0 = 0.54; a1 = 0.46; break;
+    default: break;
+  }
+  const int nth = m / 32;
+  const double th = 2.0 * kPi / (m - 1);
+  std::vector<float4> g(9 + nth);
+  g[0] = make_float4((float)(a0 - a2), (float)(-a1), (float)(2.0 * a2), 0.f);
+  for (int q = 0; q < 16; ++q) {
+    const double b = th * (2.0 * nth * q);
+    float4& e = g[1 + q / 2];
+    if (q & 1) {
+      e.z = (float)std::cos(b);
+      e.w = (float)std::sin(b);
+    } else {
+      e.x = (float)std::cos(b);
+      e.y = (float)std::sin(b);
+    }
+  }
+  for (int t = 0; t < nth; ++t)
+    g[9 + t] = make_float4((float)std::cos(th * 2 * t), (float)std::sin(th * 2 * t), (float)std::cos(th * (2 * t + 1)),
+                           (float)std::sin(th * (2 * t + 1)));
+  float4* d = nullptr;
+  int r = upload(c, &d, g);
+  if (r) return r;
+  c->wgens[key] = d;
   *out = d;
   return 0;
 }
@@ -2688,6 +2734,7 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
     std::vector<float4> w4(std::max(nb, 1));
     std::vector<float> w1(std::max(nb, 1));
     std::vector<int> base(std::max(nb, 1));
+    std::vector<float> ra(std::max(nb, 1)), rg(std::max(nb, 1));  // SpectraParams::crec's a, g
     for (int k = lo; k < hi; ++k) {
       const double f = k * df;
       double cb = std::fmod(69 + 12 * std::log2(f / 440.0), 12.0);
@@ -2702,6 +2749,9 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
       w4[k - lo] = make_float4(w[0], w[1], w[2], w[3]);
       w1[k - lo] = w[4];
       base[k - lo] = b;
+      const double u = cb - b;
+      ra[k - lo] = (float)(std::exp(-2.0 * u * u) * sw);
+      rg[k - lo] = (float)std::exp(4.0 * u);
     }
     std::vector<unsigned short> perm;
     std::vector<int> goff(13, 0);
@@ -2712,21 +2762,20 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
     }
     goff[12] = (int)perm.size();
     if (perm.empty()) perm.push_back(0);
-    std::vector<float4> rec(2 * perm.size());
+    std::vector<float> rec(3 * perm.size());
     for (size_t j = 0; j < perm.size(); ++j) {
       const int i = perm[j];
-      rec[2 * j] = w4[i];
       const int bin = lo + i;
-      float binf;
-      std::memcpy(&binf, &bin, sizeof binf);  // the bin index's bits in the record's second lane
-      rec[2 * j + 1] = make_float4(w1[i], binf, 0.f, 0.f);
+      rec[3 * j] = ra[i];
+      rec[3 * j + 1] = rg[i];
+      std::memcpy(&rec[3 * j + 2], &bin, sizeof bin);  // the bin index's bits
     }
     for (void* q : {(void*)c->ctab.w4, (void*)c->ctab.w1, (void*)c->ctab.perm, (void*)c->ctab.goff,
                     (void*)c->ctab.rec})
       if (q) (void)hipFree(q);
     c->ctab = omega_ctx::ChromaTab{};
-    HIPC(c, hipMalloc(&c->ctab.rec, rec.size() * sizeof(float4)));
-    HIPC(c, hipMemcpy(c->ctab.rec, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPC(c, hipMalloc(&c->ctab.rec, rec.size() * sizeof(float)));
+    HIPC(c, hipMemcpy(c->ctab.rec, rec.data(), rec.size() * sizeof(float), hipMemcpyHostToDevice));
     HIPC(c, hipMalloc(&c->ctab.w4, w4.size() * sizeof(float4)));
     HIPC(c, hipMalloc(&c->ctab.w1, w1.size() * sizeof(float)));
     HIPC(c, hipMalloc(&c->ctab.perm, perm.size() * sizeof(unsigned short)));
@@ -2762,6 +2811,9 @@ int omega_spectra(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t wi
   p.n = n;
   p.stride = m;
   p.win = win;
+  float4* wgen = nullptr;
+  if (m == 8192 && (e = get_wingen(c, m, window, &wgen))) return e;
+  p.wgen = wgen;
   p.mag_out = dm;
   if (bands_out) {
     p.n_out = bands->n_out;

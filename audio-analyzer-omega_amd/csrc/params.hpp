@@ -272,6 +272,7 @@ struct SpectraParams {
   const float* x;
   int64_t n, stride;       // frames of 2K samples at x + f * stride
   const float* win;        // [2K]
+  const float4* wgen;      // the window as a per-thread generator (WinGen, regfft.hpp)
   float* mag_out;          // [n, K+1] or nullptr
   // A10 (MAX op): bands [0, n_valid) of n_out, band i = max(mag[starts[i]:ends[i]]) * scale[i]
   int n_out, n_valid;
@@ -286,9 +287,11 @@ struct SpectraParams {
   const float* cw1;
   const unsigned short* cperm;
   const int* cgoff;        // [13]
-  // the same weights permuted into group order as 32-byte records {w0, w1, w2, w3 | w4, bin, -, -}
-  // (the register-FFT kernel reads record j directly: no dependent permutation load)
-  const float4* crec;      // [2 * cgoff[12]]
+  // the same bins in group order as 12-byte records {a, g, bin} for the register-FFT kernel (record j
+  // read directly: no dependent permutation load): with u = c - b the fraction of the bin's pitch class
+  // and s its octave-band scale, a = s exp(-2 u^2) and g = exp(4 u), so the five weights
+  // s exp(-2 (u - o)^2), o = -2..2, are a g^o e^{-2 o^2} (rtol 1e-5 of the chromagram: ~3e-7 here)
+  const float* crec;       // [3 * cgoff[12]]
   double* chroma_out;      // [n, 12] or nullptr (smoothed, normalised; before the temporal blend)
   const float2* tw[kMaxLog2];
 };

@@ -51,6 +51,38 @@ __device__ __forceinline__ float lane_xor1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
 
+// A cosine-sum window (np.hanning / np.hamming / np.blackman, or none) of M = 32 NTH points at the
+// register-FFT loads, where thread t takes the point pairs 2 (t + NTH q) + {0, 1}, q < 16: with
+// C_i = cos(2 pi i / (M - 1)) the window is w_i = c0 + C_i (c1 + c2 C_i), and C at the thread's points
+// is one rotation of its two base angles 2 pi (2t + e) / (M - 1) by the step 2 pi (2 NTH q) / (M - 1).
+// Table g (capi.cpp get_wingen): g[0] = {c0, c1, c2, -}, g[1 + q / 2] the steps' (cos, sin) (.xy for even
+// q, .zw for odd), g[9 + t] = {cos, sin} of the base angles for e = 0 and e = 1. Each value is within
+// ~2e-7 of the float32 window table (cos / sin rounded once each on the host, one product-difference and
+// one Horner step here) -- far inside the FFT's own float32 error -- and the frame loop reads one
+// 16-byte entry per thread instead of 16 window pairs (the per-frame window reads were ~30 KB of
+// vector-memory traffic per frame through every CU's L1; the steps are uniform scalar loads).
+struct WinGen {
+  float c0, c1, c2;
+  float4 base;
+  float4 step[8];
+  __device__ __forceinline__ WinGen(const float4* __restrict__ g, int t) {
+    const float4 c = g[0];
+    c0 = c.x;
+    c1 = c.y;
+    c2 = c.z;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) step[i] = g[1 + i];
+    base = g[9 + t];
+  }
+  template <int Q>
+  __device__ __forceinline__ float2 at() const {
+    const float4 s4 = step[Q / 2];
+    const float cs = (Q & 1) ? s4.z : s4.x, sn = (Q & 1) ? s4.w : s4.y;
+    const float C0 = fmaf(base.x, cs, -base.y * sn), C1 = fmaf(base.z, cs, -base.w * sn);
+    return make_float2(fmaf(C0, fmaf(c2, C0, c1), c0), fmaf(C1, fmaf(c2, C1, c1), c0));
+  }
+};
+
 template <int K>
 struct RegFFT {
   static_assert(K == 8192 || K == 4096, "register FFT plans: K = 4096, 8192");

@@ -189,7 +189,6 @@ __device__ __forceinline__ void mrfft_rf_body(const SpectralParams& p, int r, in
   const int64_t f = cf / p.C, c = cf % p.C;
   const ResParam& rp = p.res[r];
   const float2* x2 = reinterpret_cast<const float2*>(p.x + f * p.frame_stride + c * p.chan_stride + rp.offset);
-  const float2* w2 = reinterpret_cast<const float2*>(rp.win);
   const float2* __restrict__ twK = p.tw[ilog2(K)];
   const float2* __restrict__ twM = p.tw[ilog2(M)];
   float2 v[16];
@@ -198,6 +197,9 @@ __device__ __forceinline__ void mrfft_rf_body(const SpectralParams& p, int r, in
   float2* t2 = t2_table<K>(smem);
   FFT::fill_t2(t2, twK, t);
   asm volatile("" ::: "memory");
+  // (the window from its table: the generator of spectra_rf_body measured 0.7 us slower in the batch
+  // kernel, whose VALU costs power, than the 30 KB of L1 reads per frame it saves; round 5 A/B)
+  const float2* w2 = reinterpret_cast<const float2*>(rp.win);
   static_for<0, 16>([&](auto q) {
     const float2 a = x2[t + NTH * q], w = w2[t + NTH * q];
     v[q] = make_float2(a.x * w.x, a.y * w.y);
@@ -353,7 +355,6 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
   const int t = threadIdx.x;
   const int64_t fr = blockIdx.x;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + fr * p.stride);
-  const float2* w2 = reinterpret_cast<const float2*>(p.win);
   float2 v[16];
   const float2* __restrict__ twK = p.tw[ilog2(K)];
   const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];  // (issued before the frame: see truepeak_rf_body)
@@ -379,11 +380,12 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
     cj0 = p.cgoff[t / kGrp];
     cj1 = p.cgoff[t / kGrp + 1];
   }
+  const WinGen wg(p.wgen, t);
   asm volatile("" ::: "memory");
   OMEGA_STAMP_RT(30);
   OMEGA_STAMP(0);
   static_for<0, 16>([&](auto r) {
-    const float2 a = x2[t + NTH * r], w = w2[t + NTH * r];
+    const float2 a = x2[t + NTH * r], w = wg.template at<r>();
     v[r] = make_float2(a.x * w.x, a.y * w.y);
   });
   OMEGA_STAMP(1);
@@ -393,13 +395,13 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
   // next ones once the transform's registers are free (after the threshold barrier), so the
   // accumulation waits on no load
   constexpr int kRecPre = 2, kRecReg = 8;
-  float4 ra[kRecReg], rb[kRecReg];
+  float3 ra[kRecReg];
+  const float3* __restrict__ crec = reinterpret_cast<const float3*>(p.crec);
   int cjf = cj0 + t % kGrp;
   static_for<0, kRecPre>([&](auto i) {
     const int j = cjf + kGrp * i;
     if (j < cj1) {
-      ra[i] = p.crec[2 * j];
-      rb[i] = p.crec[2 * j + 1];
+      ra[i] = crec[j];
     }
   });
   asm volatile("" ::: "memory");
@@ -455,8 +457,7 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
     static_for<0, kRecReg>([&](auto i) {
       const int j = cjf + kGrp * i;
       if (i >= kRecPre && j < cj1) {
-        ra[i] = p.crec[2 * j];
-        rb[i] = p.crec[2 * j + 1];
+        ra[i] = crec[j];
       }
     });
   }
@@ -553,18 +554,21 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
   if (t < 12 * kGrp) {
     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     const int j1 = cj1;
-    auto acc_rec = [&](const float4 a, const float4 b) {
-      const double ed = (double)suppressed(__float_as_int(b.y));
-      acc[0] = fma(ed, (double)a.x, acc[0]);
-      acc[1] = fma(ed, (double)a.y, acc[1]);
-      acc[2] = fma(ed, (double)a.z, acc[2]);
-      acc[3] = fma(ed, (double)a.w, acc[3]);
-      acc[4] = fma(ed, (double)b.x, acc[4]);
+    auto acc_rec = [&](const float3 r) {
+      // weights of the classes b - 2 .. b + 2: a g^o e^{-2 o^2} (SpectraParams::crec)
+      const double ed = (double)suppressed(__float_as_int(r.z));
+      const float a = r.x, g = r.y, gi = __builtin_amdgcn_rcpf(g);
+      const float ag = a * g, agi = a * gi;
+      acc[0] = fma(ed, (double)(agi * (gi * 3.3546262790251185e-4f)), acc[0]);
+      acc[1] = fma(ed, (double)(agi * 1.3533528323661270e-1f), acc[1]);
+      acc[2] = fma(ed, (double)a, acc[2]);
+      acc[3] = fma(ed, (double)(ag * 1.3533528323661270e-1f), acc[3]);
+      acc[4] = fma(ed, (double)(ag * (g * 3.3546262790251185e-4f)), acc[4]);
     };
     static_for<0, kRecReg>([&](auto i) {
-      if (cjf + kGrp * i < j1) acc_rec(ra[i], rb[i]);
+      if (cjf + kGrp * i < j1) acc_rec(ra[i]);
     });
-    for (int j = cjf + kGrp * kRecReg; j < j1; j += kGrp) acc_rec(p.crec[2 * j], p.crec[2 * j + 1]);
+    for (int j = cjf + kGrp * kRecReg; j < j1; j += kGrp) acc_rec(crec[j]);
 #pragma unroll
     for (int o = 0; o < 5; ++o) part[t * 5 + o] = acc[o];
   }

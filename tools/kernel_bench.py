@@ -2,6 +2,9 @@
 """Run one stage of the cfg2 hot path in isolation (for rocprofv3 counter passes and A/B timing).
 
   python tools/kernel_bench.py {batch,tp,kw,mrfft,meters,all,host,spectra,drums,post} [--reps N]
+
+spectra-bands / spectra-chroma / spectra-mag: the cfg3 kernel with one output set only (where its LDS
+bank conflicts and time come from).
 """
 import argparse
 import os
@@ -41,7 +44,7 @@ def main():
 
     xh = bench.cfg2_input()
     host_out = {}
-    if a.stage == "spectra":
+    if a.stage.startswith("spectra"):
         from omega_gpu import Resolution
         from omega_gpu.engine import BandTable
         x3 = torch.from_numpy(bench.cfg3_input(4096, 8192)).cuda()
@@ -50,6 +53,7 @@ def main():
         bt = BandTable(e3, L.BANDS_MAX, st_, en_, 512, 4097, scale=comp_)
         so = {"bands": torch.empty(4096, 512, device="cuda"),
               "chroma": torch.empty(4096, 12, dtype=torch.float64, device="cuda")}
+        so_mag = {"mag": torch.empty(4096, 4097, device="cuda")}
 
     if a.stage == "drums":  # bench.py drums_line's call: 4096 magnitude frames x 1025 bins of one stream
         rng = np.random.default_rng(5)
@@ -84,6 +88,12 @@ def main():
                                                 ctypes.byref(part[a.stage]), L.MEM_DEVICE))
         if a.stage == "spectra":
             e3.spectra(x3, "hann", bands=bt, chroma=True, out=so)
+        if a.stage == "spectra-bands":
+            e3.spectra(x3, "hann", bands=bt, chroma=False, out={"bands": so["bands"]})
+        if a.stage == "spectra-chroma":
+            e3.spectra(x3, "hann", chroma=True, out={"chroma": so["chroma"]})
+        if a.stage == "spectra-mag":
+            e3.spectra(x3, "hann", chroma=False, mags=True, out=so_mag)
         if a.stage == "drums":
             deng.drum_features(dmag, out=dout)
         if a.stage == "post":
