@@ -4,7 +4,8 @@
   python tools/kernel_bench.py {batch,tp,kw,mrfft,meters,all,host,spectra,drums,post} [--reps N]
 
 spectra-bands / spectra-chroma / spectra-mag: the cfg3 kernel with one output set only (where its LDS
-bank conflicts and time come from).
+bank conflicts and time come from); spectra-rot: bench.py's cfg3 call, rotating over 4 distinct input
+batches (537 MB: the frames come from HBM, not the Infinity Cache).
 """
 import argparse
 import os
@@ -54,6 +55,8 @@ def main():
         so = {"bands": torch.empty(4096, 512, device="cuda"),
               "chroma": torch.empty(4096, 12, dtype=torch.float64, device="cuda")}
         so_mag = {"mag": torch.empty(4096, 4097, device="cuda")}
+        x3s = [x3] + [x3 * (1.0 + 0.125 * k) for k in range(1, 4)] if a.stage == "spectra-rot" else [x3]
+        rot = [0]
 
     if a.stage == "drums":  # bench.py drums_line's call: 4096 magnitude frames x 1025 bins of one stream
         rng = np.random.default_rng(5)
@@ -88,6 +91,9 @@ def main():
                                                 ctypes.byref(part[a.stage]), L.MEM_DEVICE))
         if a.stage == "spectra":
             e3.spectra(x3, "hann", bands=bt, chroma=True, out=so)
+        if a.stage == "spectra-rot":
+            e3.spectra(x3s[rot[0] % 4], "hann", bands=bt, chroma=True, out=so)
+            rot[0] += 1
         if a.stage == "spectra-bands":
             e3.spectra(x3, "hann", bands=bt, chroma=False, out={"bands": so["bands"]})
         if a.stage == "spectra-chroma":
