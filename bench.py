@@ -386,9 +386,14 @@ def cfg1_line(dev, reps=20, cpu=True):
     eng = Engine([Resolution((20, 20000), W1, H1, 1.0)], FS, 20000, target_bins=T, frame_size=W1,
                  device=dev.index or 0)
     out = eng.process_stream(xd, n, H1, combined=True, meters=True)
-    for _ in range(3):
-        eng.process_stream(xd, n, H1, combined=True, meters=True, out=out)
-    torch.cuda.synchronize()
+    # warm-up for >= 50 ms of wall clock: a call is ~0.1 ms of small kernels, which run at whatever
+    # shader clock the GPU is in -- after an idle gap that is the idle clock (the per-call time then
+    # read 0.21-0.27 ms instead of 0.07 ms across runs); ~30 ms of load brings the clock up
+    t_end = time.perf_counter() + 0.05
+    while time.perf_counter() < t_end:
+        for _ in range(10):
+            eng.process_stream(xd, n, H1, combined=True, meters=True, out=out)
+        torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
