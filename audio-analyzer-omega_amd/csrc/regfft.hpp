@@ -74,12 +74,14 @@ struct WinGen {
     for (int i = 0; i < 8; ++i) step[i] = g[1 + i];
     base = g[9 + t];
   }
-  template <int Q>
+  // C2 false: a two-term window (Hann, Hamming, none: c2 == 0), one FMA per point fewer
+  template <int Q, bool C2 = true>
   __device__ __forceinline__ float2 at() const {
     const float4 s4 = step[Q / 2];
     const float cs = (Q & 1) ? s4.z : s4.x, sn = (Q & 1) ? s4.w : s4.y;
     const float C0 = fmaf(base.x, cs, -base.y * sn), C1 = fmaf(base.z, cs, -base.w * sn);
-    return make_float2(fmaf(C0, fmaf(c2, C0, c1), c0), fmaf(C1, fmaf(c2, C1, c1), c0));
+    if constexpr (C2) return make_float2(fmaf(C0, fmaf(c2, C0, c1), c0), fmaf(C1, fmaf(c2, C1, c1), c0));
+    else return make_float2(fmaf(C0, c1, c0), fmaf(C1, c1, c0));
   }
 };
 
