@@ -41,6 +41,7 @@ hipError_t launch_meters(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_prep(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_query(const MeterPrepParams& p, hipStream_t s);
 hipError_t launch_meter_load(const MeterLoadParams& p, hipStream_t s);
+hipError_t launch_queue_probe(unsigned* w, unsigned target, int limit, hipStream_t side, hipStream_t main);
 hipError_t launch_bands(const BandParams& p, hipStream_t s);
 hipError_t launch_chroma(const float* spec, int64_t n, int n_bins, int lo, int hi, const double* mat, double* out,
                          hipStream_t s);
@@ -216,6 +217,10 @@ struct omega_ctx {
   hipStream_t own = nullptr, stream = nullptr;
   // fork/join streams + events for the concurrent branches, and the graph cache
   hipStream_t cap = nullptr, fork[1] = {nullptr};
+  std::vector<hipStream_t> spare;  // side streams found on the context stream's hardware queue (kept
+                                   // alive so the next one created lands on another queue)
+  unsigned* d_probe = nullptr;     // side_stream_check's two words
+  unsigned probe_seq = 0;
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   // HIP graph replay of device-memory calls: off by default -- on MI355X (ROCm 7) a replayed graph
   // put the stream layout's nodes on other queues, with ~12 us cross-queue waits and ~20 us between
@@ -1279,6 +1284,44 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   return 0;
 }
 
+// fork[0] carries the latency-bound meter kernels beside full-chip work: at the highest stream priority
+// a freed CU goes to them first
+hipError_t create_side_stream(hipStream_t* st) {
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, hi);
+  return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
+// The meter ordering needs the context's stream and fork[0] on different hardware queues (omega.h,
+// omega_set_stream), and HIP deals streams out over GPU_MAX_HW_QUEUES (4) queues per process, so with
+// other contexts or streams alive the two can share one: the batch path's device waits then run into
+// their bound (OMEGA_EHIP), and the event-joined paths serialise (bench.py's cfg1 line measured 0.28 ms
+// per call instead of 0.07 with one other context alive, tools/side_order_probe.py). Probe the pair
+// (a waiter on fork[0], then a setter on the stream: the waiter sees the value only if they run at
+// once); on a shared queue keep that side stream as a spare and take a new one -- the next queue -- and
+// probe again. Run at creation and on a stream switch.
+constexpr int kProbePolls = 8192;  // x ~0.25 us: the waiter's bound (paid only on a shared queue)
+int side_stream_check(omega_ctx* c) {
+  if (!c->d_probe) {
+    HIPC(c, hipMalloc(&c->d_probe, 2 * sizeof(unsigned)));
+    HIPC(c, hipMemset(c->d_probe, 0, 2 * sizeof(unsigned)));
+  }
+  for (int attempt = 0; attempt < 6; ++attempt) {
+    const unsigned target = ++c->probe_seq;  // (w[0] holds the previous one: never equal)
+    HIPC(c, launch_queue_probe(c->d_probe, target, kProbePolls, c->fork[0], c->stream));
+    HIPC(c, hipStreamSynchronize(c->fork[0]));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    unsigned r[2] = {0u, 0u};
+    HIPC(c, hipMemcpy(r, c->d_probe, sizeof r, hipMemcpyDeviceToHost));
+    if (r[1] == target) return 0;
+    c->spare.push_back(c->fork[0]);
+    c->fork[0] = nullptr;
+    HIPC(c, create_side_stream(&c->fork[0]));
+  }
+  return 0;  // (no independent queue found: the device waits stay bounded, omega.h)
+}
+
 // The per-batch work: layout 3 (enqueue_batch) where eligible, otherwise the full-chip kernels back to
 // back on `s` (K-weighting first); the meter aggregates' prep and LUFS query kernels (one or two
 // workgroups per channel: latency-bound) run on fork[0] beside the resolution and true-peak kernels,
@@ -1417,15 +1460,7 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) try {
   if (const char* pl = std::getenv("OMEGA_POLL_LIMIT")) c->poll_limit = std::atoi(pl) > 0 ? std::atoi(pl) : 1;
   // (the graph-capture stream is created on the first capture: a context holds two streams --
   // the hardware has GPU_MAX_HW_QUEUES = 4 queues per process, see omega.h on the meter ordering)
-  if (he == hipSuccess) {
-    // fork[0] carries the latency-bound meter kernels beside full-chip work: at the highest stream
-    // priority a freed CU goes to them first
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
-      he = hipStreamCreateWithPriority(&c->fork[0], hipStreamNonBlocking, hi);
-    else
-      he = hipStreamCreateWithFlags(&c->fork[0], hipStreamNonBlocking);
-  }
+  if (he == hipSuccess) he = create_side_stream(&c->fork[0]);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_join[0], hipEventDisableTiming);
   if (he == hipSuccess) he = hipEventCreateWithFlags(&c->ev_join[1], hipEventDisableTiming);
@@ -1437,6 +1472,7 @@ int omega_create(const omega_config* cfg, int device, omega_ctx** out) try {
   e = build_twiddles(c);
   if (!e) e = build_spectral_tables(c);
   if (!e) e = build_meter_state(c);
+  if (!e) e = side_stream_check(c);
   *out = c;
   return e;
 } catch (...) {
@@ -1914,6 +1950,8 @@ void omega_destroy(omega_ctx* c) try {
   if (c->d_tail) (void)hipFree(c->d_tail);
   for (hipStream_t st : {c->cap, c->fork[0]})
     if (st) (void)hipStreamDestroy(st);
+  for (hipStream_t st : c->spare) (void)hipStreamDestroy(st);
+  if (c->d_probe) (void)hipFree(c->d_probe);
   for (hipEvent_t ev : {c->ev_fork, c->ev_join[0], c->ev_join[1], c->ev_kw})
     if (ev) (void)hipEventDestroy(ev);
   if (c->own) (void)hipStreamDestroy(c->own);
@@ -1941,6 +1979,7 @@ int omega_set_stream(omega_ctx* c, void* s) try {
     HIPC(c, hipStreamWaitEvent(ns, c->ev_fork, 0));
     HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
     c->stream = ns;
+    if (int e = side_stream_check(c)) return e;
   }
   return 0;
 } catch (...) {

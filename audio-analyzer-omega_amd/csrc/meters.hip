@@ -157,6 +157,35 @@ __global__ __launch_bounds__(1024) void meter_load_kernel(MeterLoadParams p) {
   }
 }
 
+// Side-stream concurrency probe (capi.cpp side_stream_check): the waiter, launched first on the side
+// stream, polls (bounded) for the value the setter, launched after it on the context's stream, stores.
+// It sees it only when the two streams run on different hardware queues -- on a shared queue the setter
+// waits behind it. w[1] = target when seen, else 0.
+__global__ __launch_bounds__(64) void queue_probe_wait(unsigned* w, unsigned target, int limit) {
+  if (threadIdx.x != 0) return;
+  unsigned seen = 0u;
+  for (int i = 0; i < limit; ++i) {
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == target) {
+      seen = target;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  __hip_atomic_store(w + 1, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void queue_probe_set(unsigned* w, unsigned target) {
+  if (threadIdx.x == 0) __hip_atomic_store(w, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t launch_queue_probe(unsigned* w, unsigned target, int limit, hipStream_t side, hipStream_t main) {
+  hipLaunchKernelGGL(queue_probe_wait, dim3(1), dim3(64), 0, side, w, target, limit);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(queue_probe_set, dim3(1), dim3(64), 0, main, w, target);
+  return hipGetLastError();
+}
+
 hipError_t launch_meter_load(const MeterLoadParams& p, hipStream_t s) {
   hipLaunchKernelGGL(meter_load_kernel, dim3((unsigned)p.C), dim3(1024), 0, s, p);
   return hipGetLastError();

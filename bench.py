@@ -299,9 +299,12 @@ def cfg3_line(dev, reps=20, n_batches=4):
     st, en, comp = band_table_512()
     bt = BandTable(eng, L.BANDS_MAX, st, en, 512, m // 2 + 1, scale=comp)
     out = {"bands": torch.empty(n, 512, device=dev), "chroma": torch.empty(n, 12, dtype=torch.float64, device=dev)}
-    for k in range(n_batches):
-        eng.spectra(xs[k], "hann", bands=bt, chroma=True, out=out)
-    torch.cuda.synchronize()
+    rot = [0]
+
+    def call():
+        eng.spectra(xs[rot[0] % n_batches], "hann", bands=bt, chroma=True, out=out)
+        rot[0] += 1
+    warm_clock(call)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for i in range(reps):
@@ -386,14 +389,8 @@ def cfg1_line(dev, reps=20, cpu=True):
     eng = Engine([Resolution((20, 20000), W1, H1, 1.0)], FS, 20000, target_bins=T, frame_size=W1,
                  device=dev.index or 0)
     out = eng.process_stream(xd, n, H1, combined=True, meters=True)
-    # warm-up for >= 50 ms of wall clock: a call is ~0.1 ms of small kernels, which run at whatever
-    # shader clock the GPU is in -- after an idle gap that is the idle clock (the per-call time then
-    # read 0.21-0.27 ms instead of 0.07 ms across runs); ~30 ms of load brings the clock up
-    t_end = time.perf_counter() + 0.05
-    while time.perf_counter() < t_end:
-        for _ in range(10):
-            eng.process_stream(xd, n, H1, combined=True, meters=True, out=out)
-        torch.cuda.synchronize()
+    # (without the warm-up the per-call time read 0.21-0.27 ms on some runs instead of 0.07 ms)
+    warm_clock(lambda: eng.process_stream(xd, n, H1, combined=True, meters=True, out=out))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
@@ -429,9 +426,7 @@ def drums_line(dev, reps=20, n=4096, bins=1025):
     mags = torch.from_numpy(np.abs(rng.standard_normal((n, bins))).astype(np.float32)).to(dev)
     eng = Engine(sample_rate=FS, device=dev.index or 0)
     out = torch.empty(n, 14, dtype=torch.float64, device=dev)
-    for _ in range(3):
-        eng.drum_features(mags, out=out)
-    torch.cuda.synchronize()
+    warm_clock(lambda: eng.drum_features(mags, out=out))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
@@ -458,9 +453,7 @@ def post_line(dev, reps=20, n=4096, bins=512):
     rng = np.random.default_rng(6)
     x = torch.from_numpy(rng.random((n, bins)).astype(np.float32)).to(dev)
     pp = SpectrumPostProcessor(np.linspace(20, 20000, bins), device=dev.index or 0)
-    for _ in range(3):
-        pp.process(x)
-    torch.cuda.synchronize()
+    warm_clock(lambda: pp.process(x))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
@@ -553,6 +546,19 @@ def band_table_512(fs=FS, num_bands=512, fft_size=8192):
     """AudioProcessingPipeline band table (pipeline.py:165-230) via the product facade."""
     from omega_gpu.bands import pipeline_band_table
     return pipeline_band_table(fs, num_bands, fft_size)
+
+
+def warm_clock(fn, seconds=0.1):
+    """fn back to back for `seconds` of wall clock before a side line's timed loop. The shader clock
+    drops within milliseconds of idle and takes ~30 ms of load to come back; a side line
+    follows the host work of building its inputs and engine, and its 20 timed calls (1-6 ms) would
+    otherwise run inside the ramp -- the clock of an idle GPU, not of the continuous stream the line
+    stands for (cfg3 at continuous load: 50 us per launch at 2297 MHz, profiles/r05_power_cfg3.txt)."""
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end:
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
 
 
 def kernel_traffic(kind="batch"):
@@ -708,7 +714,8 @@ def main(argv=None):
         # true-peak role is an Infinity-Cache hit either way; this line shows what cold input costs
         x0 = prep_main[0]
         xr = [x0] + [x0 * (1.0 + 0.0625 * k) for k in range(1, 8)]
-        dtr, _, _ = measure(be, rank, world, frames, a.steps, a.warmup, gather,
+        # (800 untimed steps, ~55 ms: the clock back at the continuous-load level after building xr)
+        dtr, _, _ = measure(be, rank, world, frames, a.steps, max(a.warmup, 800), gather,
                             prep=(xr,) + tuple(prep_main[1:]))
         rotating = {"workload": f"cfg2 step over 8 distinct resident input batches rotated per step "
                                 f"({8 * frames * C * W * 4 / 2**20:.0f} MiB > the 256 MiB Infinity Cache)",

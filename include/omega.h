@@ -131,10 +131,14 @@ const char* omega_version(void);
  * and the meter prep on the context's side stream wait for each other through device counters, so the
  * two must be able to run at once. Each context owns two streams (its private one and the side stream;
  * a graph-capture stream only once graphs are enabled); HIP maps streams onto GPU_MAX_HW_QUEUES
- * hardware queues per process. Should the two share a queue, or another tenant hold every CU, the
- * wait is bounded (OMEGA_POLL_LIMIT polls): that call's meter aggregates may be stale and OMEGA_EHIP
- * is returned -- by the call itself for host memory, by the next call or omega_synchronize for
- * device memory. Layouts other than 0 order the side stream by events and carry no such condition. */
+ * hardware queues per process. omega_create and every stream switch here probe the pair (a waiter on
+ * the side stream that must see a value stored by a kernel enqueued after it on this stream) and, on a
+ * shared queue, move the side stream to a new one (the next queue), up to six times. Should that fail,
+ * or another tenant hold every CU, the wait is bounded (OMEGA_POLL_LIMIT polls): that call's meter
+ * aggregates may be stale and OMEGA_EHIP is returned -- by the call itself for host memory, by the
+ * next call or omega_synchronize for device memory. Layouts other than 0 order the side stream by
+ * events and carry no such condition (but serialise on a shared queue). A stream switch synchronises
+ * both streams once (the probe). */
 int omega_set_stream(omega_ctx* ctx, void* hip_stream);
 /* flags: bit 0 = HIP graphs: device-memory omega_process_frames calls are captured once per distinct
  * argument set and replayed afterwards (default off: measured slower than direct launches on MI355X,

@@ -711,6 +711,32 @@ def test_time_sharded_stream_meters_on_device():
         prev = D.stream_history(prev[0], prev[1], tails, world)
 
 
+def test_many_contexts_batch_meters():
+    """Contexts created one after another in one process (each holds two streams; HIP deals streams out
+    over 4 hardware queues per process): on every one of them the default batch path -- the batch kernel
+    and the side stream's meter prep ordered by device counters, which needs the two on different queues
+    (capi.cpp side_stream_check) -- returns without OMEGA_EHIP and bitwise the outputs of the first context,
+    through the context's own stream and through torch's stream."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    x = torch.from_numpy(S.cfg2_batch(32)).cuda()
+    engs, ref = [], None
+    for k in range(6):
+        e = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+        engs.append(e)
+        for _ in range(2):
+            o = e.process_frames(x, 32, 2 * 16384, 16384, meters=True)
+            e.synchronize()
+        o = {k2: v.cpu() for k2, v in o.items()}
+        if ref is None:
+            ref = o
+        for k2 in ref:
+            assert torch.equal(o[k2], ref[k2]), (k, k2)
+        # and a host-memory call (the context's own stream)
+        h = e.process_frames(x.cpu().numpy(), 32, 2 * 16384, 16384, meters=True)
+        assert np.array_equal(h["combined"], ref["combined"].numpy())
+
+
 @pytest.mark.parametrize("n_l,n_t", [(0, 0), (1, 1), (40, 40), (100, 30), (3599, 59), (2500, 0)])
 def test_meter_load_history_equals_replay(n_l, n_t):
     """omega_meter_load_history writes the meter state of a stream with the given LUFS_inst / true-peak
