@@ -1284,14 +1284,11 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   return 0;
 }
 
-// fork[0] carries the latency-bound meter kernels beside full-chip work: at the highest stream priority
-// a freed CU goes to them first
-hipError_t create_side_stream(hipStream_t* st) {
-  int lo = 0, hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
-    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, hi);
-  return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
-}
+// fork[0] carries the latency-bound meter kernels beside full-chip work, at the default priority: a
+// high-priority side stream measured the same on the cfg2 step (pipelined 65.7-68.7 vs 65.5-67.8 us,
+// profiles/r05_ab_side_priority.txt) and made the event-joined paths 2-4x slower per call with one
+// other context alive in the process (profiles/r05_side_order.txt)
+hipError_t create_side_stream(hipStream_t* st) { return hipStreamCreateWithFlags(st, hipStreamNonBlocking); }
 
 // The meter ordering needs the context's stream and fork[0] on different hardware queues (omega.h,
 // omega_set_stream), and HIP deals streams out over GPU_MAX_HW_QUEUES (4) queues per process, so with
