@@ -722,6 +722,18 @@ def main(argv=None):
                     "value": frames * C * world * a.steps / dtr, "unit": "channel-frames/s",
                     "ms_per_step": dtr / a.steps * 1e3}
         del xr
+    in_call = None
+    if not standin and not a.no_rotating and getattr(be, "pipelined", False):
+        # the same step with every call completing its own meter aggregates (no pipelining: the
+        # contract of the drop-in facades), on the headline's input
+        be.pipelined = False
+        dti, _, _ = measure(be, rank, world, frames, a.steps, max(a.warmup, 400), gather, prep=prep_main)
+        be.pipelined = True
+        be.reset()
+        in_call = {"workload": "cfg2 step with each call's meter aggregates computed in its own launch "
+                               "(omega_set_meter_pipelining off: the contract the drop-in facades use)",
+                   "value": frames * C * world * a.steps / dti, "unit": "channel-frames/s",
+                   "ms_per_step": dti / a.steps * 1e3}
     roof = None
     if not standin:
         # (right after the headline, on its input: no idle in between, see above)
@@ -773,6 +785,8 @@ def main(argv=None):
             line["cfg4"] = cfg4
         if rotating is not None:
             line["cfg2_rotating_inputs"] = rotating
+        if in_call is not None:
+            line["cfg2_meters_in_call"] = in_call
         if cfg5 is not None:
             line["cfg5"] = cfg5
         if world == 1 and not a.no_cfg3 and not standin:
