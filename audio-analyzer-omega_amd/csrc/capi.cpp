@@ -255,6 +255,10 @@ struct omega_ctx {
   // holding a CU through the batch (step 66.5-67.1 vs 67.2-67.9 us); -1: not supported, no wait
   unsigned* d_tail = nullptr;
   unsigned tail_issued = 0;
+  // (meter pipelining) the K-weighting workgroups' {generation, LUFS} words, two parities of
+  // kChunkFrames x C (KWeightParams::lufs_mirror)
+  unsigned long long* d_mirror = nullptr;
+  unsigned mirror_gen = 0;
   int tail_ok = 0;
   // device-side poll expiry flags (host-mapped: [0] meter prep, [1] join), checked by
   // check_device_err; the poll bound (OMEGA_POLL_LIMIT, a test knob)
@@ -1184,10 +1188,30 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
     // the prep on the side stream, waiting for this batch's K-weighting count
     MeterPrepParams p = mc[0];
     p.q_done = c->d_kw_done + 3;
-    kp.kw_done = c->d_kw_done;
-    c->kw_issued += (unsigned)n;
-    p.wait_ctr = c->d_kw_done;
-    p.wait_target = c->kw_issued;
+    // pipelined: the prep polls generation-tagged words the K-weighting workgroups store without a
+    // drain or a count; unpipelined: the count
+    const size_t mir_n = (size_t)kChunkFrames * c->cfg.n_channels;
+    if (fold && !c->d_mirror) {
+      HIPC(c, hipMalloc(&c->d_mirror, 2 * mir_n * sizeof(unsigned long long)));
+      HIPC(c, hipMemset(c->d_mirror, 0, 2 * mir_n * sizeof(unsigned long long)));
+    }
+    const bool mirror = fold;
+    const unsigned gen_was = c->mirror_gen;
+    if (mirror) {
+      // consecutive launches alternate parity: a prep still reading one parity while the next launch's
+      // K-weighting writes the other (it waits for nothing), and done before the launch after that
+      // (whose predecessor's segment waits for it)
+      c->mirror_gen = c->mirror_gen == 0xFFFFFFFFu ? 2u : c->mirror_gen + 1;
+      kp.lufs_mirror = c->d_mirror + (c->mirror_gen & 1) * mir_n;
+      kp.mirror_gen = c->mirror_gen;
+      p.lufs_mirror = kp.lufs_mirror;
+      p.mirror_gen = c->mirror_gen;
+    } else {
+      kp.kw_done = c->d_kw_done;
+      c->kw_issued += (unsigned)n;
+      p.wait_ctr = c->d_kw_done;
+      p.wait_target = c->kw_issued;
+    }
     if (fold && c->tail_ok == 0) {
       int ok = 0;
       HIPC(c, hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, c->device));
@@ -1221,7 +1245,9 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
         (void)hipMemcpy(c->d_kw_done, &c->kw_issued, sizeof(unsigned), hipMemcpyHostToDevice);
         c->prep_issued += (unsigned)p.C;
       } else {
-        c->kw_issued -= (unsigned)n;  // (no prep waits for this launch: nothing was enqueued)
+        // (no prep waits for this launch: nothing was enqueued; the generation goes back so the next
+        // launch takes the other parity)
+        c->mirror_gen = gen_was;
         c->seg_par[a ^ 1] = seg_par_was;  // (the pending segment stays pending)
         c->cur = cur_was;                 // (no prep writes the other parity's state)
       }
@@ -1945,6 +1971,7 @@ void omega_destroy(omega_ctx* c) try {
   drop_graphs(c);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->d_tail) (void)hipFree(c->d_tail);
+  if (c->d_mirror) (void)hipFree(c->d_mirror);
   for (hipStream_t st : {c->cap, c->fork[0]})
     if (st) (void)hipStreamDestroy(st);
   for (hipStream_t st : c->spare) (void)hipStreamDestroy(st);

@@ -254,6 +254,14 @@ __device__ __forceinline__ void gather_edges(const float (&u)[L], float* e, int 
 // With PUB, the caller's buffer (KWeightParams::lufs_copy, meter pipelining) gets a plain copy.
 template <bool PUB>
 __device__ __forceinline__ void put_lufs(const KWeightParams& p, int64_t cf, float v) {
+  if (PUB && p.lufs_mirror) {  // (pipelined: plain stores, the generation-tagged word for the prep)
+    p.lufs_out[cf] = v;
+    if (p.lufs_copy) p.lufs_copy[cf] = v;
+    __hip_atomic_store(p.lufs_mirror + cf,
+                       ((unsigned long long)p.mirror_gen << 32) | (unsigned long long)__float_as_uint(v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   if constexpr (PUB) {
     __hip_atomic_store(reinterpret_cast<unsigned*>(p.lufs_out + cf), __float_as_uint(v), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);

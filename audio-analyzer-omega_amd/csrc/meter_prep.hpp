@@ -288,7 +288,24 @@ __device__ __forceinline__ void meter_prep_body(const MeterPrepParams& p, const 
 #pragma unroll
     for (int q = 0; q < kNewCap / NTH; ++q) {
       const int f = tid * pf + q;
-      bv[q] = q < pf && f < F ? p.lufs[(int64_t)f * C + c] : -INFINITY;
+      bv[q] = -INFINITY;
+      if (q < pf && f < F) {
+        if (p.lufs_mirror) {
+          // the K-weighting workgroup's {generation, value} word (bounded poll; one 64-bit load carries
+          // both, so no fence orders anything here)
+          const unsigned long long* m = p.lufs_mirror + (int64_t)f * C + c;
+          unsigned long long w = __hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int i = 0; (unsigned)(w >> 32) != p.mirror_gen && i < p.poll_limit; ++i) {
+            __builtin_amdgcn_s_sleep(4);
+            w = __hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if ((unsigned)(w >> 32) != p.mirror_gen && p.err_word)
+            __hip_atomic_store(p.err_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          bv[q] = __uint_as_float((unsigned)w);
+        } else {
+          bv[q] = p.lufs[(int64_t)f * C + c];
+        }
+      }
     }
     auto bkey = [&](int f, float v) -> unsigned long long {
       return v > gate ? ((unsigned long long)fkey(v) << 32) | (unsigned long long)(T0 + (uint32_t)f) : ~0ull;
@@ -466,8 +483,15 @@ __device__ __forceinline__ void meter_prep_body(const MeterPrepParams& p, const 
     // earlier batch on its stream -- whose meter segment reads this buffer as its history -- ended
     for (int i = tid; i < klen; i += NTH) {
       const int src = L - klen + i;
-      p.hist_l_out[(int64_t)c * p.HL + i] =
-          src < nh ? p.hist_l_in[(int64_t)c * p.HL + src] : p.lufs[(int64_t)(src - nh) * C + c];
+      float v;
+      if (src < nh)
+        v = p.hist_l_in[(int64_t)c * p.HL + src];
+      else if (p.lufs_mirror)  // (the words polled above: this generation's, in L2)
+        v = __uint_as_float((unsigned)__hip_atomic_load(p.lufs_mirror + (int64_t)(src - nh) * C + c, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT));
+      else
+        v = p.lufs[(int64_t)(src - nh) * C + c];
+      p.hist_l_out[(int64_t)c * p.HL + i] = v;
     }
     if (tid == 0) {
       p.n_s_out[c] = Ka + Kb;

@@ -96,6 +96,10 @@ struct KWeightParams {
   // batch_kernel with meter pipelining: lufs_out is the context's staging slot the meter prep and the
   // deferred segment read, and the caller's buffer (when given) gets this copy
   float* lufs_copy;
+  // (meter pipelining) instead of the count: thread 0 also stores {mirror_gen, LUFS bits} as one 64-bit
+  // word into lufs_mirror[cf] -- no drain, no count; the meter prep polls the words for the generation
+  unsigned long long* lufs_mirror;
+  unsigned mirror_gen;
 };
 
 // Meter aggregates (meters.hip): per-channel double-buffered state (in -> out) plus per-batch scratch.
@@ -134,6 +138,10 @@ struct MeterLoadParams {
 
 struct MeterPrepParams {
   const float* lufs;    // [n_frames * C] batch instantaneous LUFS
+  // when set (meter pipelining): the batch's values come from these {generation, value} words instead of
+  // `lufs` after wait_ctr (KWeightParams::lufs_mirror): each is polled until it carries mirror_gen
+  const unsigned long long* lufs_mirror;
+  unsigned mirror_gen;
   const float* tp;      // [n_frames * C]
   int64_t n_frames;     // <= kMeterChunk per launch
   int C;
