@@ -1323,14 +1323,18 @@ hipError_t create_side_stream(hipStream_t* st) { return hipStreamCreateWithFlags
 // per call instead of 0.07 with one other context alive, tools/side_order_probe.py). Probe the pair
 // (a waiter on fork[0], then a setter on the stream: the waiter sees the value only if they run at
 // once); on a shared queue keep that side stream as a spare and take a new one -- the next queue -- and
-// probe again. Run at creation and on a stream switch.
-constexpr int kProbePolls = 8192;  // x ~0.25 us: the waiter's bound (paid only on a shared queue)
+// probe again (three times at most). Run at creation and on a stream switch.
+constexpr int kProbePolls = 2048;  // x ~0.3 us: the waiter's bound (paid only on a shared queue)
 int side_stream_check(omega_ctx* c) {
   if (!c->d_probe) {
     HIPC(c, hipMalloc(&c->d_probe, 2 * sizeof(unsigned)));
     HIPC(c, hipMemset(c->d_probe, 0, 2 * sizeof(unsigned)));
   }
-  for (int attempt = 0; attempt < 6; ++attempt) {
+  // both streams idle first: a setter queued behind earlier work on the caller's stream would read as
+  // a shared queue (a rocprofv3 trace of bench.py showed probe waiters running to their bound)
+  HIPC(c, hipStreamSynchronize(c->stream));
+  HIPC(c, hipStreamSynchronize(c->fork[0]));
+  for (int attempt = 0; attempt < 3; ++attempt) {
     const unsigned target = ++c->probe_seq;  // (w[0] holds the previous one: never equal)
     HIPC(c, launch_queue_probe(c->d_probe, target, kProbePolls, c->fork[0], c->stream));
     HIPC(c, hipStreamSynchronize(c->fork[0]));

@@ -133,7 +133,7 @@ const char* omega_version(void);
  * a graph-capture stream only once graphs are enabled); HIP maps streams onto GPU_MAX_HW_QUEUES
  * hardware queues per process. omega_create and every stream switch here probe the pair (a waiter on
  * the side stream that must see a value stored by a kernel enqueued after it on this stream) and, on a
- * shared queue, move the side stream to a new one (the next queue), up to six times. Should that fail,
+ * shared queue, move the side stream to a new one (the next queue), up to three times. Should that fail,
  * or another tenant hold every CU, the wait is bounded (OMEGA_POLL_LIMIT polls): that call's meter
  * aggregates may be stale and OMEGA_EHIP is returned -- by the call itself for host memory, by the
  * next call or omega_synchronize for device memory. Layouts other than 0 order the side stream by
