@@ -282,7 +282,7 @@ def kernel_time_ms(eng, xd, reps=20):
     return s.elapsed_time(e) / reps, ncf
 
 
-def cfg3_line(dev, reps=20, n_batches=4):
+def cfg3_line(dev, reps=100, n_batches=4):
     """BASELINE cfg3, the HBM-roofline run: 4096 mono frames x 8192 samples, fused windowed rfft ->
     512 log bands + 12-bin chromagram (omega_spectra), one launch per batch, inputs resident in HBM.
     The launches rotate over n_batches distinct input batches (134 MB each: 4 x 134 MB = 537 MB, past
@@ -375,7 +375,7 @@ def latency_line(dev, iters=1000, lufs_iters=300, cpu=True):
     return line
 
 
-def cfg1_line(dev, reps=20, cpu=True):
+def cfg1_line(dev, reps=100, cpu=True):
     """BASELINE cfg1 (configs[0], the plumbing config): one 48 kHz mono stream, hop 512, W = 1024, one
     1024-point resolution + combine(512), K-weighted LUFS + true peak + meters (momentary over 24
     frames), 600 frames of 0.5 sin(2 pi 1000 t); the whole stream in one omega_process_stream call
@@ -417,7 +417,7 @@ def cfg1_line(dev, reps=20, cpu=True):
     return line
 
 
-def drums_line(dev, reps=20, n=4096, bins=1025):
+def drums_line(dev, reps=100, n=4096, bins=1025):
     """SURVEY.md §8(f) row 1 (drum-detection features): one call over n consecutive magnitude frames
     of one stream (kick/snare band flux, adaptive thresholds, centroid), device-resident. Bytes per
     frame: the magnitude row in + 14 float64 out."""
@@ -445,7 +445,7 @@ def drums_line(dev, reps=20, n=4096, bins=1025):
                          "traffic_source": src, "bytes_per_frame": bpf}}
 
 
-def post_line(dev, reps=20, n=4096, bins=512):
+def post_line(dev, reps=100, n=4096, bins=512):
     """SURVEY.md §8(f) row 2 (the app's spectrum post-processing): one call over n consecutive
     combined spectra of one stream (equal-loudness, content type, p98 normalisation, compensation,
     band means + EMA), device-resident. Bytes per frame: the spectrum in, spectrum + bands + content out."""
