@@ -51,6 +51,64 @@ __device__ __forceinline__ float lane_xor1(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
 
+// v[m] += s * v[m] of the lane pair (lane l ^ 1), both floats of all 16 registers: one v_fmac_f32 with
+// a DPP source per float (the compiler keeps a v_mov_b32_dpp + v_fmac pair and a hazard nop). The
+// leading s_nop covers the DPP read-after-VALU-write hazard (2 wait states) for registers written
+// just before the block; inside it every instruction reads a register no earlier one wrote.
+__device__ __forceinline__ void lane_pair_fmac(float2 (&v)[16], float s) {
+  asm volatile(
+      "s_nop 1\n"
+      "v_fmac_f32_dpp %0, %0, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %1, %1, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %2, %2, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %3, %3, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %4, %4, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %5, %5, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %6, %6, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %7, %7, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %8, %8, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %9, %9, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %10, %10, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %11, %11, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %12, %12, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %13, %13, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %14, %14, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %15, %15, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %16, %16, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %17, %17, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %18, %18, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %19, %19, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %20, %20, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %21, %21, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %22, %22, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %23, %23, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %24, %24, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %25, %25, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %26, %26, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %27, %27, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %28, %28, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %29, %29, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %30, %30, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_fmac_f32_dpp %31, %31, %32 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      : "+v"(v[0].x), "+v"(v[0].y),
+        "+v"(v[1].x), "+v"(v[1].y),
+        "+v"(v[2].x), "+v"(v[2].y),
+        "+v"(v[3].x), "+v"(v[3].y),
+        "+v"(v[4].x), "+v"(v[4].y),
+        "+v"(v[5].x), "+v"(v[5].y),
+        "+v"(v[6].x), "+v"(v[6].y),
+        "+v"(v[7].x), "+v"(v[7].y),
+        "+v"(v[8].x), "+v"(v[8].y),
+        "+v"(v[9].x), "+v"(v[9].y),
+        "+v"(v[10].x), "+v"(v[10].y),
+        "+v"(v[11].x), "+v"(v[11].y),
+        "+v"(v[12].x), "+v"(v[12].y),
+        "+v"(v[13].x), "+v"(v[13].y),
+        "+v"(v[14].x), "+v"(v[14].y),
+        "+v"(v[15].x), "+v"(v[15].y)
+      : "v"(s));
+}
+
 // A cosine-sum window (np.hanning / np.hamming / np.blackman, or none) of M = 32 NTH points at the
 // register-FFT loads, where thread t takes the point pairs 2 (t + NTH q) + {0, 1}, q < 16: with
 // C_i = cos(2 pi i / (M - 1)) the window is w_i = c0 + C_i (c1 + c2 C_i), and C at the thread's points
@@ -140,12 +198,7 @@ struct RegFFT {
   }
 
   // 16-point DFT in registers, natural order out
-  static __device__ __forceinline__ void dft16(float2 (&v)[16]) {
-    dft_dif<16>(v);
-    float2 o[16];
-    static_for<0, 16>([&](auto m) { o[m] = v[brev<16>(m)]; });
-    static_for<0, 16>([&](auto m) { v[m] = o[m]; });
-  }
+  static __device__ __forceinline__ void dft16(float2 (&v)[16]) { dft16_fma(v); }
 
   // fill the pass-2 table (every thread of the workgroup; published by the first exchange's barrier)
   static __device__ __forceinline__ void fill_t2(float2* t2, const float2* __restrict__ twK, int tid) {
@@ -211,13 +264,14 @@ struct RegFFT {
       const float2* b = buf + P2R * k1 + P2C * k2 + q;
       static_for<0, 16>([&](auto r) { v[r] = b[2 * r]; });
       dft16(v);
-      // odd lanes: F1[m] * w32^m; then out = F0 + F1' (even lane), F0 - F1' (odd lane)
-      if (q) static_for<1, 16>([&](auto m) { v[m] = twc<m, 32>(v[m]); });
-      const float s = q ? -1.f : 1.f;
+      // odd lanes hold R = -w32^m F1[m] (the sign folded into the twiddle), even lanes F0[m]; then
+      // out = R + s R', R' the lane pair's value (DPP source of a v_fmac_f32): F0 + w32^m F1 on even
+      // lanes (s = -1), F0 - w32^m F1 on odd ones (s = 1) -- one instruction per float
       static_for<0, 16>([&](auto m) {
-        const float px = lane_xor1(v[m].x), py = lane_xor1(v[m].y);
-        v[m] = make_float2(fmaf(v[m].x, s, px), fmaf(v[m].y, s, py));
+        const float2 tw = twc<m + 16, 32>(v[m]);
+        v[m] = make_float2(q ? tw.x : v[m].x, q ? tw.y : v[m].y);
       });
+      lane_pair_fmac(v, q ? 1.f : -1.f);
     }
   }
 

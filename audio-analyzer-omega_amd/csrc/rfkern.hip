@@ -53,6 +53,45 @@ __device__ __forceinline__ int tp_column(int tid) {
   return a == 0 ? NTH / 2 : NTH - a;
 }
 
+// acc = max(acc, |a[m].x|, |a[m].y| over m) as 16 v_max3_f32 in one block: no canonicalization of the
+// inputs (see truepeak_rf_body) and no hazard nop between separate asm statements
+__device__ __forceinline__ void max3_abs16(float& acc, const float2 (&a)[16]) {
+  asm(
+      "v_max3_f32 %0, |%1|, |%2|, %0\n"
+      "v_max3_f32 %0, |%3|, |%4|, %0\n"
+      "v_max3_f32 %0, |%5|, |%6|, %0\n"
+      "v_max3_f32 %0, |%7|, |%8|, %0\n"
+      "v_max3_f32 %0, |%9|, |%10|, %0\n"
+      "v_max3_f32 %0, |%11|, |%12|, %0\n"
+      "v_max3_f32 %0, |%13|, |%14|, %0\n"
+      "v_max3_f32 %0, |%15|, |%16|, %0\n"
+      "v_max3_f32 %0, |%17|, |%18|, %0\n"
+      "v_max3_f32 %0, |%19|, |%20|, %0\n"
+      "v_max3_f32 %0, |%21|, |%22|, %0\n"
+      "v_max3_f32 %0, |%23|, |%24|, %0\n"
+      "v_max3_f32 %0, |%25|, |%26|, %0\n"
+      "v_max3_f32 %0, |%27|, |%28|, %0\n"
+      "v_max3_f32 %0, |%29|, |%30|, %0\n"
+      "v_max3_f32 %0, |%31|, |%32|, %0\n"
+      : "+v"(acc)
+      : "v"(a[0].x), "v"(a[0].y),
+        "v"(a[1].x), "v"(a[1].y),
+        "v"(a[2].x), "v"(a[2].y),
+        "v"(a[3].x), "v"(a[3].y),
+        "v"(a[4].x), "v"(a[4].y),
+        "v"(a[5].x), "v"(a[5].y),
+        "v"(a[6].x), "v"(a[6].y),
+        "v"(a[7].x), "v"(a[7].y),
+        "v"(a[8].x), "v"(a[8].y),
+        "v"(a[9].x), "v"(a[9].y),
+        "v"(a[10].x), "v"(a[10].y),
+        "v"(a[11].x), "v"(a[11].y),
+        "v"(a[12].x), "v"(a[12].y),
+        "v"(a[13].x), "v"(a[13].y),
+        "v"(a[14].x), "v"(a[14].y),
+        "v"(a[15].x), "v"(a[15].y));
+}
+
 template <int K>
 __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_t cf, int tid, char* smem) {
   using FFT = RegFFT<K>;
@@ -79,6 +118,8 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
     v[r] = x2[t + NTH * r];
     mx = fmaxf(mx, fmaxf(fabsf(v[r].x), fabsf(v[r].y)));
   });
+  // (formed here: sunk past the phase loop, it kept a sample pair live across it -- a spill)
+  asm volatile("" : "+v"(mx));
   OMEGA_STAMP(1);
   FFT::template run2<false, true>(v, buf, t, tid, w1, w2, t2);
   OMEGA_STAMP(2);
@@ -151,7 +192,9 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
     });
     OMEGA_STAMP(3 + 4 * P);
     FFT::template run2<true, true>(v, buf, tl, tidl, w1l, w2l, t2);
-    static_for<0, 16>([&](auto m) { fmx = fmaxf(fmx, fmaxf(fabsf(v[m].x), fabsf(v[m].y))); });
+    // max |.| by v_max3_f32 with abs modifiers, one instruction per register: the pass-3 outputs come
+    // from inline asm (RegFFT lane_pair_fmac), so fmaxf would first canonicalize every one of them
+    max3_abs16(fmx, v);
     OMEGA_STAMP(4 + 4 * P);
   }
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
