@@ -218,9 +218,12 @@ struct omega_ctx {
   // fork/join streams + events for the concurrent branches, and the graph cache
   hipStream_t cap = nullptr, fork[1] = {nullptr};
   std::vector<hipStream_t> spare;  // side streams found on the context stream's hardware queue (kept
-                                   // alive so the next one created lands on another queue)
+                                   // alive so the next one created lands on another queue; at most
+                                   // kMaxSpare, the oldest destroyed beyond that)
   unsigned* d_probe = nullptr;     // side_stream_check's two words
   unsigned probe_seq = 0;
+  std::vector<hipStream_t> checked;  // streams probed against the current fork[0] (cleared when it changes)
+  bool queue_shared = false;         // the last probe found no independent queue for fork[0]
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   // HIP graph replay of device-memory calls: off by default -- on MI355X (ROCm 7) a replayed graph
   // put the stream layout's nodes on other queues, with ~12 us cross-queue waits and ~20 us between
@@ -368,7 +371,8 @@ struct omega_ctx {
   std::vector<DevBuf> stage;
   std::vector<DevBuf> pin;
   DevBuf oarena, oarena_pin;
-  size_t oarena_used = 0, oarena_want = 0;
+  size_t oarena_used = 0, oarena_want = 0;  // the device output arena's use in this call, its wanted size
+  size_t zc_used = 0;                       // the zero-copy output buffer's use in this call
   // the call's outputs may be written by the kernels straight into the page-locked arena (set by calls
   // whose kernels only store their outputs: no output is read back by another workgroup)
   bool zc_ok = false;
@@ -884,34 +888,37 @@ int stage_in(omega_ctx* c, int slot, const void* host, size_t bytes, const void*
   return 0;
 }
 
-// Host output: a device range of the call's output arena (outs empty: the call's first output resets
-// it; an arena too small for this call is grown at the next call, this call's outputs past it use their
-// own slots). finish_host copies the arena back in one D2H copy.
+// Host output: a device range of the call's output arena, or (zc_ok) of the zero-copy buffer, each with
+// its own use counter, both reset by the call's first output. The device arena is grown, when an earlier
+// call wanted more, at this call's first output placed in it (nothing of this call is in it yet); this
+// call's outputs past its end use their own slots. finish_host copies the arena back in one D2H copy.
 template <class T>
 int stage_out(omega_ctx* c, int slot, T* host, size_t count, std::vector<HostOut>& outs, T** dev) {
   if (!host) {
     *dev = nullptr;
     return 0;
   }
+  if (outs.empty()) {
+    c->oarena_used = 0;
+    c->zc_used = 0;
+  }
   const size_t bytes = count * sizeof(T);
   if (c->zc_ok) {
     // small outputs of a store-only call: straight into page-locked memory (no copy command after the
     // kernels; finish_host only copies them to the caller's buffers on the CPU)
-    if (outs.empty()) c->oarena_used = 0;
-    const size_t off = (c->oarena_used + 255) & ~(size_t)255;
+    const size_t off = (c->zc_used + 255) & ~(size_t)255;
     if (off + bytes <= kZeroCopyOut) {
       if (!c->zc_pin.p) {
         if (int e = pinned_buf(c, c->zc_pin, kZeroCopyOut)) return e;
         HIPC(c, hipHostGetDevicePointer(&c->zc_dev, c->zc_pin.p, 0));
       }
-      c->oarena_used = off + bytes;
+      c->zc_used = off + bytes;
       outs.push_back({host, static_cast<char*>(c->zc_pin.p) + off, bytes, kZeroCopyTag + off});
       *dev = reinterpret_cast<T*>(static_cast<char*>(c->zc_dev) + off);
       return 0;
     }
   }
-  if (outs.empty()) {
-    c->oarena_used = 0;
+  if (c->oarena_used == 0) {
     if (c->oarena_want > c->oarena.n) {
       const size_t n = c->oarena_want + c->oarena_want / 4;
       if (c->oarena.p) (void)hipFree(c->oarena.p);
@@ -1324,8 +1331,13 @@ hipError_t create_side_stream(hipStream_t* st) { return hipStreamCreateWithFlags
 // (a waiter on fork[0], then a setter on the stream: the waiter sees the value only if they run at
 // once); on a shared queue keep that side stream as a spare and take a new one -- the next queue -- and
 // probe again (three times at most). Run at creation and on a stream switch.
+// A stream already probed against the current side stream is not probed again (a caller alternating
+// streams keeps its host/GPU overlap); force re-probes the pair (omega_check_queues: streams created
+// since, e.g. an RCCL communicator's, may have been dealt onto the side stream's queue).
 constexpr int kProbePolls = 2048;  // x ~0.3 us: the waiter's bound (paid only on a shared queue)
-int side_stream_check(omega_ctx* c) {
+constexpr size_t kMaxSpare = 6;
+int side_stream_check(omega_ctx* c, bool force = false) {
+  if (!force && std::find(c->checked.begin(), c->checked.end(), c->stream) != c->checked.end()) return 0;
   if (!c->d_probe) {
     HIPC(c, hipMalloc(&c->d_probe, 2 * sizeof(unsigned)));
     HIPC(c, hipMemset(c->d_probe, 0, 2 * sizeof(unsigned)));
@@ -1341,12 +1353,30 @@ int side_stream_check(omega_ctx* c) {
     HIPC(c, hipStreamSynchronize(c->stream));
     unsigned r[2] = {0u, 0u};
     HIPC(c, hipMemcpy(r, c->d_probe, sizeof r, hipMemcpyDeviceToHost));
-    if (r[1] == target) return 0;
+    if (r[1] == target) {
+      c->queue_shared = false;
+      c->checked.push_back(c->stream);
+      return 0;
+    }
+    // a new side stream: what was checked against the old one no longer holds
+    c->checked.clear();
+    if (c->spare.size() >= kMaxSpare) {
+      HIPC(c, hipStreamDestroy(c->spare.front()));
+      c->spare.erase(c->spare.begin());
+    }
     c->spare.push_back(c->fork[0]);
     c->fork[0] = nullptr;
     HIPC(c, create_side_stream(&c->fork[0]));
   }
-  return 0;  // (no independent queue found: the device waits stay bounded, omega.h)
+  // No independent queue found: not an error (the device waits stay bounded, omega.h), but reported --
+  // omega_check_queues returns it, and omega_last_error says why the batch path may return OMEGA_EHIP.
+  // The stream is not marked checked: the next switch to it probes again.
+  c->queue_shared = true;
+  std::snprintf(c->err, sizeof c->err,
+                "side stream: no hardware queue independent of the context's stream found after 3 attempts "
+                "(more streams than GPU_MAX_HW_QUEUES?): batch-path device waits may run to their bound "
+                "(OMEGA_POLL_LIMIT) and return OMEGA_EHIP");
+  return 0;
 }
 
 // The per-batch work: layout 3 (enqueue_batch) where eligible, otherwise the full-chip kernels back to
@@ -2014,6 +2044,19 @@ int omega_set_stream(omega_ctx* c, void* s) try {
   return guard_fail(c);
 }
 
+int omega_check_queues(omega_ctx* c, int* shared) try {
+  if (!c) return OMEGA_EINVAL;
+  HIPC(c, hipSetDevice(c->device));
+  if (c->pend) {  // (the probe synchronises both streams; a pending segment launches first)
+    if (int e = flush_meters(c)) return e;
+  }
+  if (int e = side_stream_check(c, true)) return e;
+  if (shared) *shared = c->queue_shared ? 1 : 0;
+  return 0;
+} catch (...) {
+  return guard_fail(c);
+}
+
 void* omega_get_stream(const omega_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
 
 int omega_get_config(const omega_ctx* c, omega_config* cfg, int* device) {
@@ -2101,9 +2144,10 @@ int omega_process_frames(omega_ctx* c, const float* x, int64_t n_frames, int64_t
   const size_t span = (size_t)((n_frames - 1) * frame_stride + (C - 1) * channel_stride + W);
   int e = 0;
   if (mem == OMEGA_MEM_HOST) {
-    // without meters every kernel of the call only stores its outputs: small ones go straight to
-    // page-locked memory (the meter path's true peaks are re-read across workgroups: device staging)
-    c->zc_ok = !meters;
+    // when every kernel of the call only stores its outputs, small ones go straight to page-locked
+    // memory: not with meters (the meter path's true peaks are re-read across workgroups) nor with combine
+    // targets owned by several resolutions (their o[t] += v reads back across kernels): device staging
+    c->zc_ok = !meters && (!comb || c->res_independent);
     e = stage_in(c, 0, x, span * sizeof(float), reinterpret_cast<const void**>(&dx));
     if (!e) e = stage_out(c, 1, comb, ncf * T, outs, &comb);
     if (!e) e = stage_out(c, 2, out->lufs_inst, ncf, outs, &lufs);
@@ -2531,8 +2575,19 @@ int omega_meter_load_history(omega_ctx* c, const float* lufs_inst, int64_t n_l, 
                              int mem) try {
   if (!c) return OMEGA_EINVAL;
   if (n_l < 0 || n_t < 0 || n_t > n_l) return fail(c, OMEGA_EINVAL, "need 0 <= n_t <= n_l");
-  if (n_l > c->HL) return fail(c, OMEGA_EINVAL, "%lld LUFS rows exceed the %d-frame history", (long long)n_l, c->HL);
   if ((n_l && !lufs_inst) || (n_t && !tp_db)) return fail(c, OMEGA_EINVAL, "null history");
+  // rows older than the windows hold (integrated_len - 1 LUFS values, peak_len - 1 true peaks) leave no
+  // trace in the state a replay of them would build: keep the last ones (a time-shard exchange hands over
+  // up to 3599 / 59 rows whatever this context's window lengths are)
+  if (n_l > c->HL) {
+    lufs_inst += (n_l - c->HL) * (int64_t)c->cfg.n_channels;
+    n_l = c->HL;
+  }
+  if (n_t > std::min<int64_t>(c->HT, n_l)) {
+    const int64_t k = std::min<int64_t>(c->HT, n_l);
+    tp_db += (n_t - k) * (int64_t)c->cfg.n_channels;
+    n_t = k;
+  }
   if (int e = check_device_err(c)) return e;
   HIPC(c, hipSetDevice(c->device));
   if (int e = flush_meters(c)) return e;  // (a pending segment reads the state being replaced)

@@ -69,6 +69,7 @@ EXPORTS = {
     "omega_destroy": (None, [C.c_void_p]),
     "omega_last_error": (C.c_char_p, [C.c_void_p]),
     "omega_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "omega_check_queues": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "omega_synchronize": (C.c_int, [C.c_void_p]),
     "omega_set_meter_pipelining": (C.c_int, [C.c_void_p, C.c_int]),
     "omega_flush_meters": (C.c_int, [C.c_void_p]),

@@ -54,11 +54,14 @@ def _ptr(a) -> Optional[int]:
 class Engine:
     def __init__(self, resolutions: Sequence[Resolution] = DEFAULT_RESOLUTIONS, sample_rate: int = 48000,
                  max_freq: float = 20000, target_bins: int = 1024, frame_size: Optional[int] = None,
-                 n_channels: int = 1, apply_weighting: bool = True, device: int = 0):
+                 n_channels: int = 1, apply_weighting: bool = True, device: int = 0,
+                 meter_windows: Optional[Sequence[int]] = None):
         self._ctx = C.c_void_p()
         cfg = L.Config()
         lib = L.lib()
         lib.omega_config_default(C.byref(cfg))
+        if meter_windows is not None:  # (momentary, short, integrated, peak) window lengths in frames
+            cfg.momentary_len, cfg.short_len, cfg.integrated_len, cfg.peak_len = (int(v) for v in meter_windows)
         resolutions = list(resolutions)
         cfg.sample_rate = int(sample_rate)
         cfg.max_freq = float(max_freq)
@@ -122,6 +125,15 @@ class Engine:
         if not tensor.is_cuda or tensor.device.index != self.device:
             raise ValueError(f"device tensor on {tensor.device}, but this engine runs on cuda:{self.device}")
         self._check(L.lib().omega_set_stream(self._ctx, C.c_void_p(torch.cuda.current_stream(tensor.device).cuda_stream)))
+
+    def check_queues(self) -> bool:
+        """Probe this context's stream and side stream again (omega_check_queues): call once other
+        components -- an RCCL communicator, another library -- have created their streams. True if the
+        two run on independent hardware queues (False: the batch path's device waits run to their
+        bound; omega_last_error says so)."""
+        shared = C.c_int(0)
+        self._check(L.lib().omega_check_queues(self._ctx, C.byref(shared)))
+        return shared.value == 0
 
     def reset_meters(self):
         self._check(L.lib().omega_meter_reset(self._ctx))

@@ -9,6 +9,7 @@ available once N_r samples were written and then sees the last N_r of them, whic
 from __future__ import annotations
 
 import logging
+import threading
 import time
 from dataclasses import dataclass
 from enum import Enum
@@ -81,6 +82,12 @@ class MultiResolutionFFT:
             FFTConfig((5000, 20000), 1024, 256, 1.5),
         ]
         self._engines: Dict[tuple, Engine] = {}
+        # process_audio_chunk and combine_results_optimized share the ring, the prepared calls and the
+        # last chunk's same-launch combine; the app may call them from different threads
+        self._lock = threading.RLock()
+        # combine target the next chunk forms in its own launch: the target_bins combine_results_optimized
+        # was last asked for (the app's display bars, omega4_main.py:714-717), 1024 until then
+        self._want_bins = 1024
         self._setup_windows()
         self._setup_buffers()
         self._setup_frequency_arrays()
@@ -111,9 +118,13 @@ class MultiResolutionFFT:
         return [Resolution(tuple(c.freq_range), c.fft_size, c.hop_size, c.weight, _win_name(c.window_type))
                 for c in self.configs]
 
+    def _cfg_key(self):
+        # everything an engine is built from: a caller may replace configs, max_freq or sample_rate
+        return (self.sample_rate, self.max_freq,
+                tuple((tuple(c.freq_range), c.fft_size, c.weight, c.window_type) for c in self.configs))
+
     def _engine(self, apply_weighting: bool, target_bins: int = 1024) -> Engine:
-        key = (apply_weighting, target_bins, tuple((c.freq_range, c.fft_size, c.weight, c.window_type)
-                                                    for c in self.configs))
+        key = (apply_weighting, target_bins, self._cfg_key())
         eng = self._engines.get(key)
         if eng is None:
             eng = Engine(self._resolutions(), self.sample_rate, self.max_freq, target_bins,
@@ -121,16 +132,15 @@ class MultiResolutionFFT:
             self._engines[key] = eng
         return eng
 
-    def _chunk_call(self, apply_weighting: bool, avail, full: bool):
-        """The per-chunk device call, prepared once per (configs, weighting, available resolutions): the
-        C ABI's output struct over persistent host arrays (the results get copies), so a call is one
-        ctypes call on the ring (host memory; omega_process_frames stages it page-locked and returns
+    def _chunk_call(self, apply_weighting: bool, avail, full: bool, target_bins: int):
+        """The per-chunk device call, prepared once per (configs, weighting, available resolutions, combine
+        target): the C ABI's output struct over persistent host arrays (the results get copies), so a call
+        is one ctypes call on the ring (host memory; omega_process_frames stages it page-locked and returns
         every output in one copy)."""
-        key = (apply_weighting, tuple(avail), full, tuple((c.freq_range, c.fft_size, c.weight, c.window_type)
-                                                           for c in self.configs))
+        key = (apply_weighting, tuple(avail), full, target_bins, self._cfg_key())
         prep = self._calls.get(key)
         if prep is None:
-            eng = self._engine(apply_weighting)
+            eng = self._engine(apply_weighting, target_bins)
             outs = L.Outputs()
             mags = {i: np.empty((1, self.configs[i].fft_size // 2 + 1), np.float32) for i in avail}
             for i, a in mags.items():
@@ -149,32 +159,37 @@ class MultiResolutionFFT:
             return {}
         try:
             start = time.perf_counter()
-            if self._wmax != max(c.fft_size for c in self.configs):
-                self._setup_buffers()
-            chunk = np.asarray(audio_chunk, dtype=np.float32).ravel()
-            ring, n = self._ring, len(chunk)
-            if n >= self._wmax:
-                ring[-self._wmax:] = chunk[-self._wmax:]
-            else:  # (in place: the ring's address stays what the prepared calls hold)
-                ring[:-n] = ring[n:]
-                ring[-n:] = chunk
-            self._written = min(self._written + n, 1 << 62)
-            avail = [i for i, c in enumerate(self.configs) if self._written >= c.fft_size]
-            results: Dict[int, FFTResult] = {}
-            self._last = None
-            if avail:
-                # with the weighted magnitudes of every resolution, the same launch also forms their
-                # combine (1024 targets, multi_resolution_fft.py:335-408): combine_results_optimized of
-                # exactly these results then needs no second device round trip
-                full = apply_weighting and len(avail) == len(self.configs)
-                eng, outs, mags, comb = self._chunk_call(apply_weighting, avail, full)
-                L.check(eng._ctx, L.lib().omega_process_frames(eng._ctx, ring.ctypes.data, 1, eng.W, eng.W,
-                                                                C.byref(outs), L.MEM_HOST))
-                for i in avail:
-                    results[i] = FFTResult(magnitude=mags[i][0].copy(), frequencies=self.freq_arrays[i],
-                                           config_index=i)
-                if full:
-                    self._last = ({i: (results[i].magnitude, mags[i][0]) for i in avail}, comb[0])
+            # (float64 frames -- the app's Hann-windowed ring slice, omega4_main.py:952-980 -- are cast
+            # by the copy into the float32 ring, not by a separate pass)
+            chunk = np.asarray(audio_chunk).ravel()
+            with self._lock:
+                if self._wmax != max(c.fft_size for c in self.configs):
+                    self._setup_buffers()
+                ring, n = self._ring, len(chunk)
+                if n >= self._wmax:
+                    ring[-self._wmax:] = chunk[-self._wmax:]
+                else:  # (in place: the ring's address stays what the prepared calls hold)
+                    ring[:-n] = ring[n:]
+                    ring[-n:] = chunk
+                self._written = min(self._written + n, 1 << 62)
+                avail = [i for i, c in enumerate(self.configs) if self._written >= c.fft_size]
+                results: Dict[int, FFTResult] = {}
+                self._last = None
+                if avail:
+                    # with the magnitudes of every resolution, the same launch also forms their combine
+                    # (multi_resolution_fft.py:335-408) for the target_bins last asked for:
+                    # combine_results_optimized of exactly these results then needs no second round trip
+                    full = len(avail) == len(self.configs)
+                    tb = self._want_bins
+                    eng, outs, mags, comb = self._chunk_call(apply_weighting, avail, full, tb)
+                    L.check(eng._ctx, L.lib().omega_process_frames(eng._ctx, ring.ctypes.data, 1, eng.W, eng.W,
+                                                                    C.byref(outs), L.MEM_HOST))
+                    for i in avail:
+                        results[i] = FFTResult(magnitude=mags[i][0].copy(), frequencies=self.freq_arrays[i],
+                                               config_index=i)
+                    if full:
+                        self._last = ({i: (results[i].magnitude, mags[i][0]) for i in avail}, comb[0], tb,
+                                      self._cfg_key())
             self.processing_stats["total_calls"] += 1
             self.processing_stats["total_time"] += time.perf_counter() - start
             return results
@@ -201,17 +216,22 @@ class MultiResolutionFFT:
             logger.warning("No FFT results to combine")
             return np.zeros(target_bins), np.linspace(0, self.max_freq, target_bins)
         try:
-            last = getattr(self, "_last", None)
-            if last is not None and target_bins == 1024 and self._same_results(results, last[0]):
-                tf = self._tfreqs.get((self.max_freq, 1024))
-                if tf is None:
-                    tf = self._tfreqs[(self.max_freq, 1024)] = np.linspace(0, self.max_freq, 1024)
-                return last[1].copy(), tf.copy()
-            target_freqs = np.linspace(0, self.max_freq, target_bins)
-            eng = self._engine(True, target_bins)
-            mags = {r.config_index: r.magnitude for r in results.values()}
-            out = eng.combine(mags, 1)
-            return out[0].copy(), target_freqs
+            with self._lock:
+                last = getattr(self, "_last", None)
+                if (last is not None and target_bins == last[2] and last[3] == self._cfg_key()
+                        and self._same_results(results, last[0])):
+                    tf = self._tfreqs.get((self.max_freq, target_bins))
+                    if tf is None:
+                        tf = self._tfreqs[(self.max_freq, target_bins)] = np.linspace(0, self.max_freq, target_bins)
+                    return last[1].copy(), tf.copy()
+                # the next chunk forms this target in its own launch
+                if isinstance(target_bins, (int, np.integer)) and target_bins > 0:
+                    self._want_bins = int(target_bins)
+                target_freqs = np.linspace(0, self.max_freq, target_bins)
+                eng = self._engine(True, target_bins)
+                mags = {r.config_index: r.magnitude for r in results.values()}
+                out = eng.combine(mags, 1)
+                return out[0].copy(), target_freqs
         except Exception as e:
             logger.error(f"FFT result combination failed: {e}")
             return np.zeros(target_bins), np.linspace(0, self.max_freq, target_bins)
@@ -232,9 +252,10 @@ class MultiResolutionFFT:
         return self.freq_arrays.copy()
 
     def reset_all_buffers(self):
-        self._ring.fill(0)
-        self._last = None
-        self._written = 0
+        with self._lock:
+            self._ring.fill(0)
+            self._last = None
+            self._written = 0
         logger.info("All buffers reset")
 
     def get_processing_stats(self) -> Dict[str, float]:

@@ -169,6 +169,13 @@ class DeviceBackend:
     def sync(self):
         torch.cuda.synchronize(self.dev)
 
+    def check_queues(self):
+        # RCCL's streams exist now (communicator init, the warmup's gathers): re-probe that the
+        # context's stream and its side stream still sit on different hardware queues
+        if not self.eng.check_queues():
+            print(f"bench.py: {self.dev}: the side stream shares a hardware queue (omega_check_queues)",
+                  file=sys.stderr)
+
 
 def prepare(be, rank, world, frames, seed_base=None):
     """The inputs and output buffers of one measurement, made ahead of it (see main: no GPU idle between
@@ -227,6 +234,8 @@ def measure(be, rank, world, frames, steps, warmup, gather, seed_base=None, prep
         step(i, 0)
     if warmup:
         drain(warmup - 1)
+    if world > 1 and hasattr(be, "check_queues"):
+        be.check_queues()
     barrier()
     t0 = time.perf_counter()
     for i in range(warmup, warmup + steps):
@@ -332,14 +341,31 @@ def latency_line(dev, iters=1000, lufs_iters=300, cpu=True):
     (a) benchmark_multi_fft (multi_resolution_fft.py:467-494: default configs, 512-sample chunks,
     process_audio_chunk + combine_results_optimized per iteration) -- the reference's only published
     on-path figure is 0.20 ms per iteration; (b) ProfessionalMetering.calculate_lufs at the app's shape
-    (omega4_main.py:1082: 2048-sample Hann-windowed float64 frames; professional_meters.py:231-281).
-    Beside each, the oracle's equivalent on this host (one core)."""
+    (omega4_main.py:1082: 2048-sample Hann-windowed float64 frames; professional_meters.py:231-281);
+    (c) the app's MRFFT call pair on those frames (app_frame_ms). Beside each, the oracle's equivalent
+    on this host (one core)."""
     from omega_gpu.multi_resolution_fft import benchmark_multi_fft
     from omega_gpu.professional_meters import ProfessionalMetering
     mr = benchmark_multi_fft(FS, 512, iters, device=dev.index or 0)
     rng = np.random.default_rng(8)
     frames = [(0.3 * np.sin(2 * np.pi * 440 * np.arange(2048) / FS + 0.1 * k) + 0.01 * rng.standard_normal(2048))
               * np.hanning(2048) for k in range(64)]
+    # (c) the app's own per-display-frame MRFFT call pair (omega4_main.py:707-717): process_audio_chunk
+    # on the 2048-sample Hann-windowed float64 frame, then combine_results_optimized at target_bins =
+    # the display bars (512): after the first frame the chunk's launch forms the 512-target combine, so
+    # the pair is one device round trip
+    from omega_gpu.multi_resolution_fft import MultiResolutionFFT
+    app = MultiResolutionFFT(FS, device=dev.index or 0)
+    for k in range(10):
+        res = app.process_audio_chunk(frames[k % 64], apply_weighting=True)
+        app.combine_results_optimized(res, target_bins=512)
+    t0 = time.perf_counter()
+    for k in range(iters):
+        res = app.process_audio_chunk(frames[k % 64], apply_weighting=True)
+        if res:
+            spectrum, freqs = app.combine_results_optimized(res, target_bins=512)
+    app_ms = (time.perf_counter() - t0) / iters * 1e3
+    app.cleanup()
     pm = ProfessionalMetering(FS, device=dev.index or 0)
     for k in range(10):
         pm.calculate_lufs(frames[k % 64])
@@ -352,7 +378,10 @@ def latency_line(dev, iters=1000, lufs_iters=300, cpu=True):
                         "float64 frames (the app's per-display-frame calls), host clock",
             "mrfft_ms_per_iteration": mr["avg_time_ms"], "mrfft_published_ms": PUBLISHED_MRFFT_MS,
             "mrfft_vs_published": PUBLISHED_MRFFT_MS / mr["avg_time_ms"],
-            "calculate_lufs_ms_per_call": lufs_ms}
+            "calculate_lufs_ms_per_call": lufs_ms,
+            "app_frame_ms": app_ms,
+            "app_frame_workload": "process_audio_chunk(2048-sample Hann float64 frame, apply_weighting=True) + "
+                                  "combine_results_optimized(target_bins=512), omega4_main.py:707-717"}
     if cpu:
         os.environ.setdefault("OMP_NUM_THREADS", "1")
         from oracle import omega_ref as R
@@ -367,6 +396,16 @@ def latency_line(dev, iters=1000, lufs_iters=300, cpu=True):
             if res:
                 R.combine(res)
         line["mrfft_oracle_ms_per_iteration"] = (time.perf_counter() - t0) / n * 1e3
+        st = R.MRFFTStream()
+        for k in range(10):
+            st.process(frames[k % 64])
+        n = max(100, iters // 5)
+        t0 = time.perf_counter()
+        for k in range(n):
+            res = st.process(frames[k % 64])
+            if res:
+                R.combine(res, target_bins=512)
+        line["app_frame_oracle_ms"] = (time.perf_counter() - t0) / n * 1e3
         ms = R.MeterState(FS)
         t0 = time.perf_counter()
         for k in range(lufs_iters):
@@ -679,6 +718,7 @@ def main(argv=None):
             dist.init_process_group(be.dist_backend)
         else:
             dist.init_process_group(be.dist_backend, device_id=be.dev)
+            be.check_queues()
     gather = world > 1 and not a.no_gather
 
     frames = a.frames

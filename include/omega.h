@@ -133,13 +133,21 @@ const char* omega_version(void);
  * a graph-capture stream only once graphs are enabled); HIP maps streams onto GPU_MAX_HW_QUEUES
  * hardware queues per process. omega_create and every stream switch here probe the pair (a waiter on
  * the side stream that must see a value stored by a kernel enqueued after it on this stream) and, on a
- * shared queue, move the side stream to a new one (the next queue), up to three times. Should that fail,
+ * shared queue, move the side stream to a new one (the next queue), up to three times (each distinct
+ * stream once; omega_check_queues re-probes). Should that fail,
  * or another tenant hold every CU, the wait is bounded (OMEGA_POLL_LIMIT polls): that call's meter
  * aggregates may be stale and OMEGA_EHIP is returned -- by the call itself for host memory, by the
  * next call or omega_synchronize for device memory. Layouts other than 0 order the side stream by
  * events and carry no such condition (but serialise on a shared queue). A stream switch synchronises
  * both streams once (the probe). */
 int omega_set_stream(omega_ctx* ctx, void* hip_stream);
+/* Probe the context's stream and its side stream again, whatever was probed before (a stream switch
+ * probes each distinct stream once): streams created since -- an RCCL communicator's, another library's
+ * -- may share a hardware queue with the side stream. Moves the side stream as omega_set_stream does;
+ * *shared (optional) = 1 if no independent queue was found (the device waits then run to their bound;
+ * omega_last_error says so), else 0. Synchronises both streams (a pending meter segment launches
+ * first). Not part of the reference surface: the multi-GPU host calls it once its collectives exist. */
+int omega_check_queues(omega_ctx* ctx, int* shared);
 /* flags: bit 0 = HIP graphs: device-memory omega_process_frames calls are captured once per distinct
  * argument set and replayed afterwards (default off: measured slower than direct launches on MI355X,
  * see DESIGN.md); bits 1-2 = stream layout:
@@ -223,7 +231,8 @@ int omega_meter_reset(omega_ctx* ctx);
  * frame following them: what omega_meter_reset + omega_meter_update over those n_l frames (the true
  * peaks of the n_l - n_t older ones -100 dBTP) leave, written by one kernel without computing their
  * aggregates (a time-sharded stream's rank loads the history before its shard; SURVEY §8(e),
- * omega_gpu/dist.py meter_time_shard). n_l <= integrated_len - 1. Replaces the reference's deques
+ * omega_gpu/dist.py meter_time_shard). Rows beyond the windows (n_l > integrated_len - 1, n_t >
+ * peak_len - 1) are older than anything the state keeps: the last ones are used. Replaces the reference's deques
  * (professional_meters.py:20-25) filled by calculate_lufs calls. */
 int omega_meter_load_history(omega_ctx* ctx, const float* lufs_inst, int64_t n_l, const float* tp_db, int64_t n_t,
                              int mem);

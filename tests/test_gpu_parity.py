@@ -106,6 +106,42 @@ def test_mrfft_combine_reuse_needs_unmodified_results(mr):
     np.testing.assert_array_equal(c3, fresh.combine_results_optimized(copied, 1024)[0])
 
 
+def test_mrfft_combine_reuse_follows_target_bins(mr):
+    """The app's call pair (omega4_main.py:707-717: a float64 Hann-windowed frame, then the combine at
+    target_bins = its display bars): the first combine at 512 targets runs on the device from the values
+    given and makes every later chunk form the 512-target combine in its own launch; that cached result
+    is returned only for the unmodified results of the last chunk, equals the combine kernel's, and
+    follows the reference to SPEC_TOL. A max_freq change after the chunk invalidates it."""
+    m = _mrfft()
+    x = mr["triad_4096/x"]
+    x64 = np.asarray(x, np.float64)
+    res = m.process_audio_chunk(x64)
+    c0, f0 = m.combine_results_optimized(res, 512)  # (the combine kernel; the target is now 512)
+    assert normwise(c0, mr["triad_4096/comb512"]) < SPEC_TOL
+    np.testing.assert_allclose(f0, mr["triad_4096/tgt512"])
+    res = m.process_audio_chunk(x64)
+    assert m._last is not None and m._last[2] == 512  # formed in the chunk's launch
+    c1, f1 = m.combine_results_optimized(res, 512)
+    assert normwise(c1, mr["triad_4096/comb512"]) < SPEC_TOL
+    np.testing.assert_array_equal(f1, f0)
+    fresh = _mrfft()
+    c2, _ = fresh.combine_results_optimized(res, 512)
+    np.testing.assert_allclose(c1, c2, rtol=1e-6, atol=1e-7)
+    res[2].magnitude[:] *= 2.0  # modified: combined from the values given
+    c3, _ = m.combine_results_optimized(res, 512)
+    np.testing.assert_array_equal(c3, fresh.combine_results_optimized(res, 512)[0])
+    res = m.process_audio_chunk(x64)
+    m.max_freq = 16000.0  # configuration changed after the chunk: no stale reuse
+    c4, f4 = m.combine_results_optimized(res, 512)
+    assert f4[-1] == 16000.0
+    np.testing.assert_array_equal(c4, _mrfft_maxf(16000.0).combine_results_optimized(res, 512)[0])
+
+
+def _mrfft_maxf(mf):
+    from omega_gpu.multi_resolution_fft import MultiResolutionFFT
+    return MultiResolutionFFT(FS, max_freq=mf)
+
+
 SMALL = [((20, 2000), 256, 128, 1.5), ((200, 6000), 128, 64, 1.2), ((1000, 12000), 64, 32, 1.0),
          ((5000, 20000), 512, 256, 1.5)]
 
@@ -735,6 +771,71 @@ def test_many_contexts_batch_meters():
         # and a host-memory call (the context's own stream)
         h = e.process_frames(x.cpu().numpy(), 32, 2 * 16384, 16384, meters=True)
         assert np.array_equal(h["combined"], ref["combined"].numpy())
+
+
+def test_side_stream_reprobed_with_busy_streams():
+    """An RCCL-like neighbour: four more streams created after the context, each with a long-running
+    kernel in flight (torch.cuda._sleep), then omega_check_queues re-probes the pair (capi.cpp
+    side_stream_check) and in-call and pipelined batches with meters run beside them: no OMEGA_EHIP, and
+    every output bitwise what the same sequence gives on a quiet context."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    x = torch.from_numpy(S.cfg2_batch(32)).cuda()
+
+    def sequence(e):
+        got = []
+        for pipe in (False, True, False):
+            e.set_meter_pipelining(pipe)
+            for _ in range(2):
+                o = e.process_frames(x, 32, 2 * 16384, 16384, meters=True)
+                e.flush_meters()
+                got.append({k: v.clone() for k, v in o.items()})
+        e.synchronize()
+        return [{k: v.cpu() for k, v in o.items()} for o in got]
+
+    quiet = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+    ref = sequence(quiet)
+    quiet.close()
+    e = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    for st in streams:
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(20_000_000)  # ~10 ms each, in flight while the batches run
+    independent = e.check_queues()
+    got = sequence(e)
+    torch.cuda.synchronize()
+    assert isinstance(independent, bool)
+    for a, b in zip(ref, got):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+    # a switch back to an already-probed stream does not probe again, and the context keeps working
+    with torch.cuda.stream(streams[0]):
+        o = e.process_frames(x, 32, 2 * 16384, 16384, meters=False)
+    torch.cuda.synchronize()
+    assert torch.equal(o["combined"].cpu(), ref[0]["combined"])
+
+
+def test_meter_load_history_longer_than_windows():
+    """A context with shorter meter windows (integrated 600 frames, true peak 30) handed the time-shard
+    exchange's full 3599 / 59-row history: omega_meter_load_history keeps the rows its windows hold, and
+    the shard metered after it is bitwise what the replay of every row gives."""
+    import torch
+    from omega_gpu import Engine, Resolution
+    from omega_gpu import dist as D
+    rng = np.random.default_rng(11)
+    hl = torch.from_numpy(rng.uniform(-90, -5, (3599, 2)).astype(np.float32)).cuda()
+    ht = torch.from_numpy(rng.uniform(-40, 0, (59, 2)).astype(np.float32)).cuda()
+    sl = torch.from_numpy(rng.uniform(-80, -5, (300, 2)).astype(np.float32)).cuda()
+    st = torch.from_numpy(rng.uniform(-40, 0, (300, 2)).astype(np.float32)).cuda()
+    kw = dict(sample_rate=FS, max_freq=20000, target_bins=2, frame_size=512, n_channels=2,
+              meter_windows=(24, 180, 600, 30))
+    a, b = (Engine([Resolution((20, 20000), 512, 256, 1.0)], **kw) for _ in range(2))
+    got = D.meter_time_shard(a, sl, st, (hl, ht))
+    b.reset_meters()
+    rl, rt = D.history_frames(hl, ht)
+    b.meter_update(rl.contiguous(), rt.contiguous(), rl.shape[0])
+    ref = b.meter_update(sl, st, 300)
+    assert torch.equal(got, ref)
 
 
 @pytest.mark.parametrize("n_l,n_t", [(0, 0), (1, 1), (40, 40), (100, 30), (3599, 59), (2500, 0)])
