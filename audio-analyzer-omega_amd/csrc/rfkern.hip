@@ -195,6 +195,19 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
     // max |.| by v_max3_f32 with abs modifiers, one instruction per register: the pass-3 outputs come
     // from inline asm (RegFFT lane_pair_fmac), so fmaxf would first canonicalize every one of them
     max3_abs16(fmx, v);
+#if defined(OMEGA_EXP_STALL)  // energy-vs-stall experiment, never in the product:
+    // idle issue cycles per phase and wave, no VALU
+    asm volatile("s_sleep %0" ::"i"(OMEGA_EXP_STALL));
+#endif
+#if defined(OMEGA_EXP_VALU)  // the converse: 4 x OMEGA_EXP_VALU FMAs on dead registers, four independent chains
+    {
+      float d0 = fmx, d1 = mx, d2 = fmx + 1.f, d3 = mx + 1.f;
+      asm volatile(".rept %4\n v_fma_f32 %0, %0, %5, %6\n v_fma_f32 %1, %1, %5, %6\n"
+                   " v_fma_f32 %2, %2, %5, %6\n v_fma_f32 %3, %3, %5, %6\n .endr"
+                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3)
+                   : "i"(OMEGA_EXP_VALU), "v"(0.5f), "v"(0.25f));
+    }
+#endif
     OMEGA_STAMP(4 + 4 * P);
   }
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
