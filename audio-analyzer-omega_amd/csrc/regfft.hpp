@@ -328,6 +328,69 @@ struct RegFFT {
     __syncthreads();
   }
 
+  // ---- half-buffer form (K = 4096: the cfg3 kernel at five workgroups per CU) ----
+  // Every exchange moves the real parts, then the imaginary parts, through ONE float buffer of kSlots
+  // floats (17,408 B instead of 34,816): same slot maps in float units -- rows of P1 = 272 floats, so
+  // ds_read_b32 / ds_write_b32 lane groups of 32 stay conflict-free (P1 = P2R = 16 mod 32; P2C = 17 pairs
+  // every k2 with a distinct bank in each half-row; the natural-order map's XOR leaves the 32 lanes of a
+  // group on 32 banks) -- at two more barriers per workgroup exchange and twice the LDS instructions.
+  // The exchange-2 rows stay this wave's own (no barrier), as in run2.
+  template <bool LT2 = false>
+  static __device__ __forceinline__ void run_half(float2 (&v)[16], float* bf, int t, float2 w1, float2 w2,
+                                                  const float2* t2 = nullptr) {
+    static_assert(L == 16, "the half-buffer plan is K = 4096");
+    dft16(v);
+    twiddle(v, w1);
+    const int u = t % L, k1 = t / L;
+    // exchange 1: real parts, barrier, read; barrier (every real read done), imaginary parts, read
+    {
+      float* b = bf + t;
+      static_for<0, 16>([&](auto j) { b[P1 * j] = v[j].x; });
+    }
+    __syncthreads();
+    {
+      const float* b = bf + P1 * k1 + u;
+      static_for<0, 16>([&](auto r) { v[r].x = b[L * r]; });
+    }
+    __syncthreads();
+    {
+      float* b = bf + t;
+      static_for<0, 16>([&](auto j) { b[P1 * j] = v[j].y; });
+    }
+    __syncthreads();
+    {
+      const float* b = bf + P1 * k1 + u;
+      static_for<0, 16>([&](auto r) { v[r].y = b[L * r]; });
+    }
+    dft16(v);
+    if constexpr (LT2)
+      twiddle_t2(v, t2 + u);
+    else
+      twiddle(v, w2);
+    // exchange 2 (this wave's rows; LDS operations of a wave complete in issue order)
+    {
+      float* bw = bf + P2R * k1 + u;
+      static_for<0, 16>([&](auto j) { bw[P2C * j] = v[j].x; });
+    }
+    wave_lds_sync();
+    const int k2 = t & 15, k1b = t >> 4;
+    const float* br = bf + P2R * k1b + P2C * k2;
+    static_for<0, 16>([&](auto r) { v[r].x = br[r]; });
+    {
+      float* bw = bf + P2R * k1 + u;
+      static_for<0, 16>([&](auto j) { bw[P2C * j] = v[j].y; });
+    }
+    wave_lds_sync();
+    static_for<0, 16>([&](auto r) { v[r].y = br[r]; });
+    dft16(v);
+  }
+  // natural-order slots of the pass-3 outputs, one component (the caller synchronises around it)
+  template <bool IM>
+  static __device__ __forceinline__ void store_spectrum_half(const float2 (&v)[16], float* bf, int t) {
+    float* b = bf + s3o(t);
+    static_for<0, 16>([&](auto m) { b[o3o(m)] = IM ? v[m].y : v[m].x; });
+  }
+
   // Natural-order spectrum exchange after run(): every register to its frequency's slot
   // (the caller synchronises before, if the buffer may still be read, and after).
   static __device__ __forceinline__ void store_spectrum(const float2 (&v)[16], float2* buf, int t) {

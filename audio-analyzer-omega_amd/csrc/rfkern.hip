@@ -380,11 +380,31 @@ hipError_t launch_mrfft_rf(int n, const SpectralParams& p, int r, hipStream_t s)
 }
 
 // Fused spectrum analysis (cfg3: A13 -> A10 + A12, see spectra.hip for the reference mapping) on the
-// register FFT: one 256-thread workgroup per frame of 2K samples, four workgroups per CU (36 KiB of
-// LDS each: the exchange buffer, reused for the contiguous magnitudes and the chroma partials; the
-// band and chroma tables are read from global memory, L1/L2-resident).
+// register FFT: one 256-thread workgroup per frame of 2K samples, FIVE workgroups per CU (<= 32,000 B
+// of LDS and <= 96 VGPRs each): the transform's exchanges move real and imaginary parts in turn through
+// one 17 KiB float buffer (RegFFT::run_half), reused after the transform for the contiguous magnitudes,
+// the chroma partials and the peak flags (~28 KiB); the band and chroma tables are read from global
+// memory, L1/L2-resident.
 constexpr int kSpecRfThreads = 256;
+#ifndef OMEGA_SPEC_WGS
+#define OMEGA_SPEC_WGS 5  // workgroups per CU the LDS and register budgets are sized for (6: 59 vs 50.5 us, r06)
+#endif
+constexpr int kSpecRfWgs = OMEGA_SPEC_WGS;
 constexpr int kSpecRfPeakWords = 12;  // peaks among bins < 64 * 12 = 768: suppression reaches k / 2 < 1536 / 2
+template <int K>
+struct SpecRfLds {
+  static constexpr size_t kT2Off = RegFFT<K>::kSlots * sizeof(float);  // pass-2 twiddles after the exchange
+  static constexpr size_t kXform = kT2Off + RegFFT<K>::kT2 * sizeof(float2);
+  static constexpr size_t kPartOff = ((K + 1) * sizeof(float) + 15) / 16 * 16;
+  static constexpr size_t kClsOff = kPartOff + 240 * 5 * sizeof(float);
+  static constexpr size_t kRedOff = kClsOff + 12 * 5 * sizeof(double);
+  static constexpr size_t kFlagOff = (kRedOff + (RegFFT<K>::NTH / 64) * sizeof(float) + 15) / 16 * 16;
+  static constexpr int kFlagWords = 2 * 64 * kSpecRfPeakWords / 4;  // one suppression byte per bin < c_hi
+  static constexpr size_t kPost = kFlagOff + kFlagWords * sizeof(unsigned);
+  static constexpr size_t kBytes = kXform > kPost ? kXform : kPost;
+  // the LDS is handed out in 1280-byte granules of the CU's 160 KiB
+  static_assert((kBytes + 1279) / 1280 * 1280 * kSpecRfWgs <= 160 * 1024, "LDS of kSpecRfWgs workgroups per CU");
+};
 
 
 template <int K>
@@ -393,21 +413,16 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
   constexpr int NTH = FFT::NTH;
   static_assert(NTH == kSpecRfThreads, "one 256-thread workgroup per frame");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // the exchange buffer; after the transform it holds the magnitudes, the chroma partials, the peak
-  // bitmap and the reduction scratch
-  float2* buf = reinterpret_cast<float2*>(smem);
+  // the exchange buffer (floats: RegFFT::run_half); after the transform it holds the magnitudes, the
+  // chroma partials, the peak bitmap and the reduction scratch
+  using Lds = SpecRfLds<K>;
+  float* bf = reinterpret_cast<float*>(smem);
   float* magc = reinterpret_cast<float*>(smem);  // |X_k|, k <= K, once the untangle is done
-  constexpr size_t kPartOff = ((K + 1) * sizeof(float) + 15) / 16 * 16;
-  constexpr size_t kClsOff = kPartOff + 240 * 5 * sizeof(double);
-  constexpr size_t kRedOff = kClsOff + 12 * 5 * sizeof(double);
-  constexpr size_t kFlagOff = (kRedOff + (NTH / 64) * sizeof(float) + 15) / 16 * 16;
-  constexpr int kFlagWords = 2 * 64 * kSpecRfPeakWords / 4;  // one suppression byte per bin < c_hi
-  static_assert(kFlagOff + kFlagWords * sizeof(unsigned) <= FFT::kSlots * sizeof(float2),
-                "magnitudes, chroma partials and scratch fit the exchange buffer");
-  double* part = reinterpret_cast<double*>(smem + kPartOff);  // [240][5]
-  double(*cls)[5] = reinterpret_cast<double(*)[5]>(smem + kClsOff);
-  float* redf = reinterpret_cast<float*>(smem + kRedOff);
-  unsigned* sflag = reinterpret_cast<unsigned*>(smem + kFlagOff);
+  constexpr int kFlagWords = Lds::kFlagWords;
+  float* part = reinterpret_cast<float*>(smem + Lds::kPartOff);  // [240][5] (the threads' float sums)
+  double(*cls)[5] = reinterpret_cast<double(*)[5]>(smem + Lds::kClsOff);
+  float* redf = reinterpret_cast<float*>(smem + Lds::kRedOff);
+  unsigned* sflag = reinterpret_cast<unsigned*>(smem + Lds::kFlagOff);
   const int t = threadIdx.x;
   const int64_t fr = blockIdx.x;
   const float2* x2 = reinterpret_cast<const float2*>(p.x + fr * p.stride);
@@ -415,8 +430,8 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
   const float2* __restrict__ twK = p.tw[ilog2(K)];
   const float2 w1 = twK[t], w2b = twK[16 * (t % FFT::L)];  // (issued before the frame: see truepeak_rf_body)
   const float2 wm = p.tw[ilog2(2 * K)][t];
-  // pass-2 twiddle table after the exchange buffer and its slack (RegFFT::fill_t2)
-  float2* t2 = reinterpret_cast<float2*>(smem + (FFT::kSlots + 8) * sizeof(float2));
+  // pass-2 twiddle table after the exchange buffer (RegFFT::fill_t2)
+  float2* t2 = reinterpret_cast<float2*>(smem + Lds::kT2Off);
   FFT::fill_t2(t2, twK, t);
   // this thread's band-table entries (bands t, t + NTH) and chroma-group bounds, issued with the
   // twiddles ahead of the frame: their latency is off the band / chroma phases' critical path
@@ -452,7 +467,7 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
     });
   }
   OMEGA_STAMP(1);
-  FFT::template run<false, true>(v, buf, t, w1, w2b, t2);
+  FFT::template run_half<true>(v, bf, t, w1, w2b, t2);
   OMEGA_STAMP(2);
   // this thread's chroma records (group-ordered, j = cjf + kGrp i): the first two issued now, the
   // next ones once the transform's registers are free (after the threshold barrier), so the
@@ -468,22 +483,40 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
     }
   });
   asm volatile("" ::: "memory");
-  __syncthreads();
-  FFT::store_spectrum(v, buf, t);
-  __syncthreads();
-  OMEGA_STAMP(3);
   // Each untangle of the pair (k, K - k) gives both bins: thread t takes the pairs k = t + NTH q, q < 8
   // (k < K/2) -- bins k in mg[q], K - k = K - t - NTH q in mgm[q] (t = 0, q = 0: bin 0 and the Nyquist
   // bin K) -- and thread 0 the self-mirrored K/2 as well: half the untangles and half the mirror
-  // reads of one untangle per bin.
+  // reads of one untangle per bin. The natural-order spectrum goes through the float buffer as real
+  // parts, then imaginary parts (the registers a round frees take the values it reads).
+  float ax[8], bx[8], ay[8], by[8];
+  float hx = 0.f, hy = 0.f;
+  {
+    const float* bo = bf + FFT::s3(t);
+    const float* bm = bf + FFT::s3m(t);
+    __syncthreads();  // every exchange-2 read is done
+    FFT::template store_spectrum_half<false>(v, bf, t);
+    __syncthreads();
+    static_for<0, 8>([&](auto q) {
+      ax[q] = bo[FFT::o3(q)];
+      bx[q] = bm[FFT::o3(15 - q)];
+    });
+    if (t == 0) hx = bo[FFT::o3(8)];
+    __syncthreads();
+    FFT::template store_spectrum_half<true>(v, bf, t);
+    __syncthreads();
+    static_for<0, 8>([&](auto q) {
+      ay[q] = bo[FFT::o3(q)];
+      by[q] = bm[FFT::o3(15 - q)];
+    });
+    if (t == 0) hy = bo[FFT::o3(8)];
+  }
+  OMEGA_STAMP(3);
   float mg[8], mgm[8];
   float mx = 0.f, mhalf = 0.f;
   {
-    const float2* bo = buf + FFT::s3(t);
-    const float2* bm = buf + FFT::s3m(t);
     static_for<0, 8>([&](auto q) {
-      const float2 a = bo[FFT::o3(q)];
-      const float2 b = bm[FFT::o3(15 - q)];
+      const float2 a = make_float2(ax[q], ay[q]);
+      const float2 b = make_float2(bx[q], by[q]);
       float2 xk, xkk;
       untangle(a, b, twc<q, 32>(wm), xk, xkk);
       mg[q] = cabs(xk);
@@ -497,7 +530,7 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
       mx = fmaxf(mx, fmaxf(mg[q], mgm[q]));
     });
     if (t == 0) {
-      mhalf = cabs(bo[FFT::o3(8)]);  // X[K/2] = conj(Z[K/2])
+      mhalf = cabs(make_float2(hx, hy));  // X[K/2] = conj(Z[K/2])
       mx = fmaxf(mx, mhalf);
     }
   }
@@ -635,7 +668,7 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
     });
     for (int j = cjf + kGrp * kRecReg; j < j1; j += kGrp) acc_rec(crec[j]);
 #pragma unroll
-    for (int o = 0; o < 5; ++o) part[t * 5 + o] = (double)acc[o];
+    for (int o = 0; o < 5; ++o) part[t * 5 + o] = acc[o];
   }
   OMEGA_STAMP(9);
   __syncthreads();
@@ -644,7 +677,7 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
     const int g = t / 5, o = t % 5;
     double sgo = 0.0;
 #pragma unroll
-    for (int r = 0; r < kGrp; ++r) sgo += part[(g * kGrp + r) * 5 + o];
+    for (int r = 0; r < kGrp; ++r) sgo += (double)part[(g * kGrp + r) * 5 + o];
     cls[(g + o + 10) % 12][o] = sgo;
   }
   __syncthreads();
@@ -664,7 +697,7 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
 }
 
 template <int K>
-__global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraParams p) {
+__global__ __launch_bounds__(kSpecRfThreads, kSpecRfWgs) void spectra_rf_kernel(SpectraParams p) {
   OMEGA_WG_BEGIN();
   spectra_rf_body<K>(p);
   OMEGA_WG_END(20);
@@ -673,9 +706,8 @@ __global__ __launch_bounds__(kSpecRfThreads, 4) void spectra_rf_kernel(SpectraPa
 hipError_t launch_spectra_rf(int m, const SpectraParams& p, hipStream_t s) {
   // a suppressed bin k < c_hi names bin k / h >= k / 2, which must lie in the peak bitmap
   if (m != 8192 || (p.chroma_out && p.c_hi > 2 * 64 * kSpecRfPeakWords)) return hipErrorInvalidValue;
-  using FFT = RegFFT<4096>;
-  const size_t lds = (FFT::kSlots + 8 + FFT::kT2) * sizeof(float2);
-  hipLaunchKernelGGL(spectra_rf_kernel<4096>, dim3((unsigned)p.n), dim3(kSpecRfThreads), lds, s, p);
+  hipLaunchKernelGGL(spectra_rf_kernel<4096>, dim3((unsigned)p.n), dim3(kSpecRfThreads), SpecRfLds<4096>::kBytes,
+                     s, p);
   return hipGetLastError();
 }
 

@@ -40,6 +40,10 @@ PEAK_HBM_GBS = 8000.0
 FLOP_TP = 2.5 * W * np.log2(W) + 2.5 * 4 * W * np.log2(4 * W) + 8 * W          # 3.33 MFLOP (reference algorithm)
 FLOP_FFT = sum(2.5 * n * np.log2(n) + 3.5 * n for n in (16384, 8192, 4096, 1024))  # 1.09 MFLOP
 FLOP_KW = 4 * (W + 18) * 9 + 5 * W                                                 # 0.67 MFLOP
+# the true peak as the kernel executes it (polyphase form, rfkern.hip): four K = W/2-point complex FFTs
+# (5 K log2 K each: the forward rfft and three phase inverses), three phase rotations + Hermitian packs
+# (16 flops per bin), one untangle (10 per bin) -- 2.60 MFLOP against the reference algorithm's 3.33
+FLOP_TP_EXEC = 4 * 5 * (W // 2) * np.log2(W // 2) + 3 * 16 * (W // 2) + 10 * (W // 2)
 BYTES_CF = 4 * W + 4 * (T + 2)                                                     # 67,592 B
 METRIC = "audio frames/sec (multi-res FFT + LUFS + TruePeak) at 1/2/4/8 MI355X"
 
@@ -786,6 +790,13 @@ def main(argv=None):
                 "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
                 "kernel_ms": kt_ms, "flop_per_launch": flop_launch,
+                "executed": {"flop_per_launch": (FLOP_FFT + FLOP_KW + FLOP_TP_EXEC) * kcf,
+                             "achieved": (FLOP_FFT + FLOP_KW + FLOP_TP_EXEC) * kcf / (kt_ms * 1e-3) / 1e12,
+                             "frac": (FLOP_FFT + FLOP_KW + FLOP_TP_EXEC) * kcf / (kt_ms * 1e-3) / 1e12
+                             / PEAK_FP32_TFLOPS,
+                             "note": "the flops the kernel executes: the true peak in its polyphase form "
+                                     "(FLOP_TP_EXEC, 2.60 M per channel-frame) instead of the reference's "
+                                     "resample algorithm; frac above is SURVEY.md §8(d)'s count"},
                 "traffic_unit": "bytes per launch (HBM, FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": kcf * BYTES_CF,

@@ -48,6 +48,12 @@ def test_natural_order_4096_separable_forms():
     assert s3(256) + 256 * 15 == 4096 < 4352
 
 
+def test_half_buffer_layout():
+    """RegFFT<4096>::run_half: the same maps in float units through one 4352-float buffer, every access a
+    32-lane ds_read_b32 / ds_write_b32 -- conflict-free except one extra cycle on the mirror reads."""
+    _check(M.HalfPlan4096(), 4352, ("x3m",))
+
+
 def test_tight_layout():
     pl = M.TightPlan4096()
     _check(pl, 4096)

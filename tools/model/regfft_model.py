@@ -151,6 +151,31 @@ class TightPlan4096(Plan):
         return n ^ ((n >> 4) & 15)
 
 
+class HalfPlan4096(Plan):
+    """RegFFT<4096>::run_half (the cfg3 kernel at five workgroups per CU): the padded K = 4096 slot maps
+    in FLOAT units, real parts then imaginary parts through one buffer of 4352 floats; every exchange
+    access is ds_read_b32 / ds_write_b32 (2 x 32 lanes, bank = float index mod 32)."""
+
+    def __init__(self):
+        super().__init__(4096)
+
+    def check_conflicts(self):
+        K, NTH, L = self.K, self.NTH, self.L
+        r32 = lambda a: conflicts(a, 32, 32)  # noqa: E731  (both instructions: groups of 32, mod 32)
+        worst = {}
+        for w in range(NTH // 64):
+            lanes = [w * 64 + l for l in range(64)]
+            for r in range(16):
+                worst["x1w"] = max(worst.get("x1w", 0), r32([self.a1(t, r) for t in lanes]))
+                worst["x1r"] = max(worst.get("x1r", 0), r32([self.a1(self.p2(t)[0] + L * r, self.p2(t)[1]) for t in lanes]))
+                worst["x2w"] = max(worst.get("x2w", 0), r32([self.a2(self.p2(t)[0], r, self.p2(t)[1]) for t in lanes]))
+                worst["x2r"] = max(worst.get("x2r", 0), r32([self.a2(r, self.p3(s)[1], self.p3(s)[2]) for s in lanes]))
+                worst["x3w"] = max(worst.get("x3w", 0), r32([self.a3(self.out_index(s, r)) for s in lanes]))
+                worst["x3r"] = max(worst.get("x3r", 0), r32([self.a3(t + NTH * r) for t in lanes]))
+                worst["x3m"] = max(worst.get("x3m", 0), r32([self.a3((K - t - NTH * r) % K) for t in lanes]))
+        return worst
+
+
 def check_tight():
     pl = TightPlan4096()
     rng = np.random.default_rng(1)
