@@ -151,8 +151,9 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
   }
   float2 y[16];
   static_for<0, 16>([&](auto r) { y[r] = v[r]; });
-  // i e^{2 pi i t / M} / 2: alpha_k = (1/2, 0) + (that) e^{2 pi i r / 32}
-  const float2 hz = make_float2(0.5f * wm.y, 0.5f * wm.x);
+  // i e^{2 pi i t / M}: 2 alpha_k = (1, 0) + (that) e^{2 pi i r / 32} -- the phases' transforms take
+  // 2 Z'_k (one multiply fewer per bin), their maxima are halved at the end
+  const float2 hz = make_float2(wm.y, wm.x);
   float fmx = 0.f;
   // byte address of the lane holding the mirror column (itself for columns 0 and NTH / 2)
   const int lane = tid & 63;
@@ -185,10 +186,10 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
       } else {
         if (tl == 0) yp = cconj(y[16 - r]);
       }
-      const float2 g = twc<-r, 32>(hzl);  // (i e_t / 2) e^{2 pi i r / 32}
-      const float2 al = make_float2(0.5f + g.x, g.y);
-      const float2 d = csub(y[r], yp);
-      v[r] = cconj(cadd(yp, cmul(al, d)));
+      // 2 Z'_k = conj(S + g D), S = Y_k + Y', D = Y_k - Y', g = (i e_t) e^{2 pi i r / 32}
+      const float2 g = twc<-r, 32>(hzl);
+      const float2 S = cadd(y[r], yp), D = csub(y[r], yp);
+      v[r] = make_float2(fmaf(g.x, D.x, fmaf(-g.y, D.y, S.x)), fmaf(-g.x, D.y, fmaf(-g.y, D.x, -S.y)));
     });
     OMEGA_STAMP(3 + 4 * P);
     FFT::template run2<true, true>(v, buf, tl, tidl, w1l, w2l, t2);
@@ -210,7 +211,7 @@ __device__ __forceinline__ void truepeak_rf_body(const SpectralParams& p, int64_
 #endif
     OMEGA_STAMP(4 + 4 * P);
   }
-  const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
+  const float peak = block_max<NTH>(fmaxf(mx, fmx * (0.5f / K)), red, tid);
   if (tid == 0) {
     const float db = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
     if (p.tp_done) {  // write-through, drained, then counted in (see SpectralParams::tp_done)

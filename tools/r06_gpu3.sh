@@ -5,9 +5,9 @@ set -u -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "spectra or chroma or bands or cfg3" > gpurun_out/r06_spec_tests.txt 2>&1 || { tail -40 gpurun_out/r06_spec_tests.txt; exit 1; }
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "${TK:-spectra or chroma or bands or cfg3}" > gpurun_out/r06_spec_tests.txt 2>&1 || { tail -40 gpurun_out/r06_spec_tests.txt; exit 1; }
 tail -2 gpurun_out/r06_spec_tests.txt
-CHECK=0 ROUNDS=3 STAGES=spectra,spectra-rot AB_LIBS=${AB:-libomega_r5.so} timeout -k 10 400 tools/ab.sh > gpurun_out/ab_spec.txt 2>&1 || exit 1
+CHECK=0 ROUNDS=3 STAGES=${STAGES:-spectra,spectra-rot} AB_LIBS=${AB:-libomega_r5.so} timeout -k 10 400 tools/ab.sh > gpurun_out/ab_spec.txt 2>&1 || exit 1
 cat gpurun_out/ab_spec.txt
 timeout -k 10 120 python tools/wgtrace.py --cfg3 --trace > gpurun_out/wgtrace_cfg3.txt 2>&1 || { tail -5 gpurun_out/wgtrace_cfg3.txt; exit 1; }
 head -30 gpurun_out/wgtrace_cfg3.txt
