@@ -2640,8 +2640,22 @@ int omega_calculate_lufs(omega_ctx* c, const float* x, int64_t n_frames, int32_t
     if (!dl) dl = c->d_lufs_scr;
     if (!dt) dt = c->d_lufs_scr + ncf;
   }
+  // The weighting and the true peak read the same input and write different outputs: the true peak
+  // runs on the side stream beside the weighting's latency-bound float64 scans (per-call metering of
+  // the app's 2048-sample frames: 37 + 14 us of kernels in sequence before), both joined before the
+  // aggregates (whose ordering against the side stream omega_meter_update keeps as always).
+  HIPC(c, hipEventRecord(c->ev_fork, c->stream));
+  HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
+  {
+    const hipStream_t main = c->stream;
+    c->stream = c->fork[0];
+    e = omega_true_peak_os(c, dx, ncf, m, oversampling, dt, OMEGA_MEM_DEVICE);
+    c->stream = main;
+    if (e) return e;
+  }
   if ((e = omega_weighting(c, dx, ncf, m, mode, nullptr, dl, OMEGA_MEM_DEVICE))) return e;
-  if ((e = omega_true_peak_os(c, dx, ncf, m, oversampling, dt, OMEGA_MEM_DEVICE))) return e;
+  HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
+  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[0], 0));
   if ((e = omega_meter_update(c, dl, dt, n_frames, dm, OMEGA_MEM_DEVICE))) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
