@@ -72,8 +72,8 @@ __device__ __forceinline__ void mv4(const float4 m, float a0, float a1, float& r
 // the last sample to the first (the last thread first, each chunk from its end). pro(): the state
 // entering the first processed sample (the odd-extension prologue: a serial, wave-uniform chain) --
 // evaluated by wave 0 only and handed to the other waves through LDS with the pass's one barrier. On
-// return u holds the outputs and (fin0, fin1) the state after the last processed sample (all
-// threads). pwl[l] = P^(l+1) (LDS). sh: >= 4*NW + 4 floats of LDS; the forward and the backward pass
+// return u holds the outputs and (fin0, fin1) the state after the last processed sample (in wave 0 of a
+// forward pass, the one place it is used: the backward pass's prologue). pwl[l] = P^(l+1) (LDS). sh: >= 4*NW + 4 floats of LDS; the forward and the backward pass
 // use separate parts, so the pass needs a single barrier.
 template <int L, int NTH, bool REV, int SB, bool OPQ = false, class Pro>
 __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, const float4* pwl, Pro pro, float* sh,
@@ -150,19 +150,25 @@ __device__ __forceinline__ void lfilter_pass(float (&u)[L], const BqRegs& t, con
   }
   __syncthreads();
   OMEGA_STAMP(SB + 2);
-  const float sin0 = sio[0], sin1 = sio[1];
-  float c0 = sin0, c1 = sin1, k0 = sin0, k1 = sin1;
-  static_for<0, NW>([&](auto w) {
-    if (w == vw) {
-      k0 = c0;
-      k1 = c1;
-    }
+  // The carry into this wave: the chain over the waves before it in processing order -- a wave-uniform
+  // trip count (no per-lane select over all NW steps) -- and, in the one wave that needs it (wave 0 of a
+  // forward pass: its final state starts the backward pass's prologue), on over the rest to the pass's
+  // final state. (Every lane of every wave used to run all NW steps: ~40 VALU per pass and thread.)
+  float c0 = sio[0], c1 = sio[1];
+  const int nwv = __builtin_amdgcn_readfirstlane(vw);
+  const int nend = __builtin_amdgcn_readfirstlane((!REV && wv == 0) ? NW : vw);
+  auto step = [&](int w) {
     float r0, r1;
     mv4(t.p64, c0, c1, r0, r1);
     c0 = r0 + shp[2 * w];
     c1 = r1 + shp[2 * w + 1];
-  });
-  fin0 = c0;
+  };
+#pragma unroll 1
+  for (int w = 0; w < nwv; ++w) step(w);
+  const float k0 = c0, k1 = c1;
+#pragma unroll 1
+  for (int w = nwv; w < nend; ++w) step(w);
+  fin0 = c0;  // (the pass's final state in forward wave 0; what the caller ignores elsewhere)
   fin1 = c1;
   // 4) true end state of this chunk and the incoming state
   {
