@@ -674,12 +674,17 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
   OMEGA_STAMP(9);
   __syncthreads();
   OMEGA_STAMP(10);
-  if (t < 60) {  // group g, offset o -> class (g + o - 2) mod 12
-    const int g = t / 5, o = t % 5;
-    double sgo = 0.0;
+  // group g, offset o -> class (g + o - 2) mod 12: the pair's 20 partials summed by a lane quad of
+  // every wave (five each, then two butterfly steps) instead of one lane's serial chain of 20
+  if (t < 60 * 4) {
+    const int pr = t >> 2, k = t & 3, g = pr / 5, o = pr % 5;
+    const float* pp = part + (g * kGrp + 5 * k) * 5 + o;
+    double sgo = (double)pp[0];
 #pragma unroll
-    for (int r = 0; r < kGrp; ++r) sgo += (double)part[(g * kGrp + r) * 5 + o];
-    cls[(g + o + 10) % 12][o] = sgo;
+    for (int r = 1; r < 5; ++r) sgo += (double)pp[5 * r];
+    sgo += __shfl_xor(sgo, 1, 64);
+    sgo += __shfl_xor(sgo, 2, 64);
+    if (k == 0) cls[(g + o + 10) % 12][o] = sgo;
   }
   __syncthreads();
   if (t < 64) {  // class sums, 3-tap circular smoothing and normalisation in one wave
@@ -689,8 +694,11 @@ __device__ __forceinline__ void spectra_rf_body(const SpectraParams& p) {
     const double chm = cls[cm][0] + cls[cm][1] + cls[cm][2] + cls[cm][3] + cls[cm][4];
     const double chp = cls[cp][0] + cls[cp][1] + cls[cp][2] + cls[cp][3] + cls[cp][4];
     const double sm = 0.25 * chm + 0.5 * ch + 0.25 * chp;
-    double tot = 0.0;
-    for (int q = 0; q < 12; ++q) tot += __shfl(sm, q, 64);
+    double tot = t < 12 ? sm : 0.0;  // the 12 classes' sum over lanes 0..15 by a butterfly
+    tot += __shfl_xor(tot, 8, 64);
+    tot += __shfl_xor(tot, 4, 64);
+    tot += __shfl_xor(tot, 2, 64);
+    tot += __shfl_xor(tot, 1, 64);
     if (t < 12) p.chroma_out[fr * 12 + c] = tot > 0 ? sm / tot : sm;
   }
   OMEGA_STAMP(11);
