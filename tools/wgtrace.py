@@ -188,6 +188,11 @@ def main():
             col = qm[:, k]
             print(f"  meter role {lab:>20}: min {np.nanmin(col):6.1f}  p50 {np.nanmedian(col):6.1f}  "
                   f"max {np.nanmax(col):6.1f} us")
+        for k, lab in ((5, "window sums + count"), (6, "extras pass done"), (7, "percentiles done")):
+            col = qm[:, k]  # (marks inside meter_query_wave, when the build records them)
+            if np.any(np.isfinite(col)):
+                print(f"  meter role {lab:>20}: min {np.nanmin(col):6.1f}  p50 {np.nanmedian(col):6.1f}  "
+                      f"max {np.nanmax(col):6.1f} us")
         for r, lab in ((0, "kw"), (1, "tp")):
             if np.any(role == r):
                 print(f"  last {lab} workgroup ends at {end[role == r].max():6.1f} us")
