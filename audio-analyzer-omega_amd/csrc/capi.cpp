@@ -1100,7 +1100,8 @@ bool batch_eligible(omega_ctx* c, const SpectralParams& sp, const KWeightParams&
 // The default layout for 16384-sample frames. On `s`: one batch_kernel launch (BatchPlan: K-weighting
 // and 16384-point-resolution workgroups mixed, then the true peaks, then the small resolutions, then --
 // for a batch of at most kChunkFrames frames per channel -- the meter aggregates as the grid's last
-// segment). On fork[0]: the meter prep (it waits on the K-weighting count, kw_done, and counts itself
+// segment; pipelined, the previous call's, between the true peaks and the small resolutions). On
+// fork[0]: the meter prep (it waits on the K-weighting count, kw_done, and counts itself
 // in). The meter workgroups wait for the prep's count and for the true peaks' count, so `s` completes
 // only after fork[0]'s work: no stream events and no kernel after the batch (each event record / wait
 // cost ~7-13 us of idle GPU between kernels). Longer batches (chunks chained through the per-context
@@ -1172,12 +1173,22 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   bp.seg_start[1] = bp.seg_begin[1];
   bp.multi_start = bp.seg_begin[2];
   const int64_t body_end = end + nwg;
-  // the grid's last segment (measured: placed before the small resolutions it holds 64 slots from
-  // ~50 us on and the step is no shorter, 77.4-79.2 vs 77.0-78.0 us); pipelined, it waits for nothing
-  // and fills the slots the tail leaves idle (first in the grid it delayed the true peaks: step 68-69
-  // vs 64-65 us without meters)
+  // the grid's last segment unpipelined (measured: placed before the small resolutions it holds 64
+  // slots from ~50 us on while it waits and the step is no shorter, 77.4-79.2 vs 77.0-78.0 us);
+  // pipelined, it waits for nothing (first in the grid it delayed the true peaks: step 68-69 vs 64-65
+  // us without meters)
   bp.q_begin = (int)body_end;
   bp.q_n = (int)q_n;
+  // pipelined (the previous call's segment: it waits for nothing), the segment goes after the true peaks
+  // and before the small resolutions instead: longest-first in the tail, its ~9-10 us workgroups ahead
+  // of the 7-12 us resolution ones (pipelined step 62.6-64.6 vs 63.9-65.9 us, four alternations on one
+  // box, tools/ab.sh, outputs bitwise equal; after the 8192-point resolution 63.2-65.4)
+  if (fold) bp.q_begin = bp.multi_start;
+#ifdef OMEGA_Q_AFTER_SEG  // (A/B builds: after small-resolution segment OMEGA_Q_AFTER_SEG - 1; 0: last)
+  if (fold) bp.q_begin = OMEGA_Q_AFTER_SEG > 0 && bp.multi.n_seg >= OMEGA_Q_AFTER_SEG
+                             ? bp.multi_start + (OMEGA_Q_AFTER_SEG < bp.multi.n_seg ? bp.multi.wg_begin[OMEGA_Q_AFTER_SEG] : (int)nwg)
+                             : (int)body_end;
+#endif
   // (measured, round 5: the pipelined segment between segment 0 and the true peaks instead, step
   // 65.3-67.1 vs 66.5-66.6 us on one box: no difference)
   const int64_t grid = body_end + q_n;

@@ -772,9 +772,11 @@ __device__ __forceinline__ void batch_kw_role(const KWeightParams& kp, int64_t c
   kw_count_in(kp, tid);
 }
 
-// Meter role (workgroup q of the nq of the meter segment, the grid's last): wave w computes outputs
-// o = 8 q + w, 8 q + w + 8 nq, ... = (frame o / C, channel o % C). The workgroups are dispatched after
-// every other role of the batch, so their waits cannot hold back the batch work they wait for: first
+// Meter role (workgroup q of the nq of the meter segment): wave w computes outputs o = 8 q + w,
+// 8 q + w + 8 nq, ... = (frame o / C, channel o % C). Unpipelined the segment is the grid's last: its
+// workgroups are dispatched after every other role of the batch, so their waits cannot hold back the
+// batch work they wait for (pipelined, the previous call's segment waits for nothing and is dispatched
+// after the true peaks, ahead of the small resolutions: capi.cpp enqueue_batch): first
 // (bounded) until the meter prep kernel on the side stream has counted in (it has waited for the
 // batch's K-weighting count), then the LUFS meters; then until every true-peak workgroup has counted
 // in, then the true-peak meter and the roll of the true-peak history. The batch completes only
@@ -867,7 +869,10 @@ __device__ __forceinline__ void batch_body(const SpectralParams& sp, const KWeig
     return;
   }
   const MultiPlan& mp = bp.multi;
-  const int w = b - bp.multi_start;
+  // (the meter segment may sit before or inside the small resolutions: the workgroups after it shift by
+  // q_n)
+  const int w = b - bp.multi_start -
+                (b >= bp.q_begin + bp.q_n && bp.q_begin < bp.multi_start + bp.multi_n ? bp.q_n : 0);
   if (w < 0 || w >= bp.multi_n) return;
   int s = 0;
   while (s + 1 < mp.n_seg && w >= mp.wg_begin[s + 1]) ++s;

@@ -1,4 +1,4 @@
-"""Outputs of one build over three consecutive cfg2 batches with meters (and a 4096-frame cfg4 shard),
+"""Outputs of one build over three consecutive cfg2 batches with meters, direct and pipelined (and a 1500-frame cfg4 shard),
 saved for a bitwise comparison between builds (tools/ab.sh: a scheduling variant must not change a
 single bit). Development tool: --lib picks another build in lib/."""
 import argparse
@@ -27,6 +27,15 @@ for i in range(3):
     o = eng.process_frames(x[256 * i:256 * (i + 1)], 256, 2 * 16384, 16384, meters=True)
     for k, v in o.items():
         res[f"{k}{i}"] = v.cpu().numpy()
+# the same batches through a pipelined context (each call's meter segment runs in the next launch):
+# every output, including the deferred meters once flushed
+eng = Engine(NORTHSTAR_RESOLUTIONS, 48000, 20000, target_bins=512, n_channels=2)
+eng.set_meter_pipelining(True)
+outs = [eng.process_frames(x[256 * i:256 * (i + 1)], 256, 2 * 16384, 16384, meters=True) for i in range(3)]
+eng.synchronize()
+for i, o in enumerate(outs):
+    for k, v in o.items():
+        res[f"{k}{i}_pipe"] = v.cpu().numpy()
 x4 = torch.from_numpy(S.cfg2_batch(1500, seed_l=4, seed_r=5)).cuda()
 o = Engine(NORTHSTAR_RESOLUTIONS, 48000, 20000, target_bins=512, n_channels=2).process_frames(
     x4, 1500, 2 * 16384, 16384, meters=True)
