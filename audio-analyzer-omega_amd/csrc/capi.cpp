@@ -1181,14 +1181,12 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
   bp.q_n = (int)q_n;
   // pipelined (the previous call's segment: it waits for nothing), the segment goes after the true peaks
   // and before the small resolutions instead: longest-first in the tail, its ~9-10 us workgroups ahead
-  // of the 7-12 us resolution ones (pipelined step 62.6-64.6 vs 63.9-65.9 us, four alternations on one
-  // box, tools/ab.sh, outputs bitwise equal; after the 8192-point resolution 63.2-65.4)
+  // of the 7-12 us resolution ones (pipelined step 63.5-64.4 vs 64.9-65.2 us last, four alternations on
+  // one box, tools/ab.sh, outputs bitwise equal direct and pipelined; on a second box 62.8-64.7 vs
+  // 64.6-65.1 last and 62.8-64.4 after the 8192-point resolution).
+  // Unpipelined it stays last: before the small resolutions its waiting workgroups cost the in-call
+  // step 70.4-73.1 vs 66.9-67.6 us
   if (fold) bp.q_begin = bp.multi_start;
-#ifdef OMEGA_Q_AFTER_SEG  // (A/B builds: after small-resolution segment OMEGA_Q_AFTER_SEG - 1; 0: last)
-  if (fold) bp.q_begin = OMEGA_Q_AFTER_SEG > 0 && bp.multi.n_seg >= OMEGA_Q_AFTER_SEG
-                             ? bp.multi_start + (OMEGA_Q_AFTER_SEG < bp.multi.n_seg ? bp.multi.wg_begin[OMEGA_Q_AFTER_SEG] : (int)nwg)
-                             : (int)body_end;
-#endif
   // (measured, round 5: the pipelined segment between segment 0 and the true peaks instead, step
   // 65.3-67.1 vs 66.5-66.6 us on one box: no difference)
   const int64_t grid = body_end + q_n;
