@@ -241,6 +241,9 @@ struct omega_ctx {
   unsigned tp_issued = 0;         // batch true-peak workgroups launched with the count on (d_kw_done[2])
   unsigned prep_issued = 0;       // meter prep workgroups launched with the count on (d_kw_done[3])
   unsigned seg_issued = 0;        // meter-segment workgroups launched (they count in at d_kw_done[4])
+  unsigned lt_issued = 0;         // omega_calculate_lufs true-peak workgroups (they count in at d_kw_done[5])
+  unsigned* tp_count_to = nullptr;  // set inside omega_calculate_lufs: its true peaks count in here
+  bool side_meters = false;  // meter kernels enqueued on fork[0] since omega_calculate_lufs last joined it
   // seg_issued once the last meter segment that reads parity p's scratch / state has counted in: the
   // preps' targets before they overwrite them (MeterPrepParams::seg_ctr)
   unsigned seg_par[2] = {0, 0};
@@ -807,7 +810,7 @@ int build_meter_state(omega_ctx* c) {
     HIPC(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->d_err), c->h_err, 0));
   }
   HIPC(c, hipMemset(c->d_kw_done, 0, 8 * sizeof(unsigned)));
-  c->kw_issued = c->q_issued = c->tp_issued = c->prep_issued = c->seg_issued = 0;
+  c->kw_issued = c->q_issued = c->tp_issued = c->prep_issued = c->seg_issued = c->lt_issued = 0;
   c->seg_par[0] = c->seg_par[1] = 0;
   c->pend = false;
   return omega_meter_reset(c);
@@ -1041,9 +1044,15 @@ std::vector<MeterPrepParams> meter_chunks(omega_ctx* c, const float* lufs, const
 // All meter chunks on one stream. tp_ready: when set, an event the true peaks of the batch wait on
 // (the prep kernels only read the LUFS_inst values, so they may start before it).
 int meters_enqueue(omega_ctx* c, const float* lufs, const float* tp, int64_t n_frames, double* out,
-                   hipStream_t stream, hipEvent_t tp_ready) {
+                   hipStream_t stream, hipEvent_t tp_ready, unsigned* wait_ctr = nullptr, unsigned wait_target = 0) {
   bool first = true;
-  for (const MeterPrepParams& p : meter_chunks(c, lufs, tp, n_frames, out)) {
+  for (MeterPrepParams p : meter_chunks(c, lufs, tp, n_frames, out)) {
+    // (wait_ctr: the first chunk's prep polls it before reading the batch's values -- the true peaks
+    // of omega_calculate_lufs on the side stream counting in, instead of an event join)
+    if (first && wait_ctr) {
+      p.wait_ctr = wait_ctr;
+      p.wait_target = wait_target;
+    }
     HIPC(c, launch_meter_prep(p, stream));
     if (tp_ready && first) HIPC(c, hipStreamWaitEvent(stream, tp_ready, 0));
     HIPC(c, launch_meter_query(p, stream));
@@ -1244,6 +1253,7 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
     // waits for it); pipelined: after it, behind the stream wait -- enqueued before the batch, a wait
     // whose stream shared a hardware queue with the batch's would block the batch behind it for ever
     if (!fold) HIPC(c, launch_meter_prep(p, c->fork[0]));
+    c->side_meters = true;
     mq = mc[0];
     mq.start_ctr = c->d_kw_done + 3;
     mq.start_target = c->prep_issued + (unsigned)p.C;
@@ -1275,6 +1285,7 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
       ++c->tail_issued;
     }
     if (fold) HIPC(c, launch_meter_prep(p, c->fork[0]));
+    c->side_meters = true;
     c->prep_issued += (unsigned)p.C;
     if (fold) {
       if (c->pend) c->seg_issued += (unsigned)c->pend_nq;
@@ -1299,9 +1310,11 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
         p.wait_target = c->kw_issued;
       }
       HIPC(c, launch_meter_prep(p, c->fork[0]));
+    c->side_meters = true;
       p.parts = 1;
       p.q_done = c->d_kw_done + 1;
       HIPC(c, launch_meter_query(p, c->fork[0]));
+      c->side_meters = true;
       c->q_issued += (unsigned)(((p.n_frames + 3) / 4) * p.C);  // (counted once it is enqueued)
     }
   }
@@ -1425,8 +1438,10 @@ int enqueue_frames(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int
     HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_kw, 0));
     for (MeterPrepParams p : mc) {
       HIPC(c, launch_meter_prep(p, c->fork[0]));
+    c->side_meters = true;
       p.parts = 1;
       HIPC(c, launch_meter_query(p, c->fork[0]));
+      c->side_meters = true;
     }
     HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
   }
@@ -2425,6 +2440,7 @@ int omega_true_peak_os(omega_ctx* c, const float* x, int64_t n, int32_t m, int32
   if (e) return e;
   sp.rot = rot;
   sp.tp_phases = oversampling == 4 ? 0xE : (oversampling == 2 ? 0x4 : 0);
+  sp.tp_done = c->tp_count_to;  // (omega_calculate_lufs)
   HIPC(c, tp_launch(c, m, sp, c->stream));
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
@@ -2545,6 +2561,26 @@ int omega_weighting(omega_ctx* c, const float* x, int64_t n, int32_t m, int32_t 
   return guard_fail(c);
 }
 
+// The meter aggregates on the caller's stream from device inputs. join_side: these kernels read the
+// state a meter prep on the side stream may still be writing (after its count-in), so the caller's
+// stream first waits for the side stream (a caller that has just joined it skips the second wait);
+// order_side: the next batch's meter prep runs on the side stream and reads, before its K-weighting
+// count, the state these kernels write, so the side stream is ordered after them (a host-memory
+// caller does it after its copies back, which then follow the kernels without an event between).
+int meter_update_dev(omega_ctx* c, const float* dl, const float* dt, int64_t n_frames, double* dm, bool join_side,
+                     bool order_side, unsigned* wait_ctr = nullptr, unsigned wait_target = 0) {
+  if (join_side) {
+    HIPC(c, hipEventRecord(c->ev_join[1], c->fork[0]));
+    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[1], 0));
+  }
+  if (int e = meters_enqueue(c, dl, dt, n_frames, dm, c->stream, nullptr, wait_ctr, wait_target)) return e;
+  if (order_side) {
+    HIPC(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
+  }
+  return 0;
+}
+
 int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db, int64_t n_frames, double* meters,
                        int mem) try {
   if (!c || !lufs_inst || !tp_db || !meters) return OMEGA_EINVAL;
@@ -2564,16 +2600,7 @@ int omega_meter_update(omega_ctx* c, const float* lufs_inst, const float* tp_db,
     if (!e) e = stage_out(c, 4, meters, ncf * 5, outs, &dm);
     if (e) return e;
   }
-  // these kernels run on the caller's stream and read the state a meter prep on the side stream may
-  // still be writing (after its count-in): the caller's stream waits for the side stream first
-  HIPC(c, hipEventRecord(c->ev_join[1], c->fork[0]));
-  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[1], 0));
-  e = meters_enqueue(c, dl, dt, n_frames, dm, c->stream, nullptr);
-  if (e) return e;
-  // the next batch's meter prep runs on the side stream and reads, before its K-weighting count, the
-  // state these kernels write on the caller's stream: order the side stream after them
-  HIPC(c, hipEventRecord(c->ev_fork, c->stream));
-  HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
+  if ((e = meter_update_dev(c, dl, dt, n_frames, dm, true, true))) return e;
   if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
   return 0;
 } catch (...) {
@@ -2651,22 +2678,52 @@ int omega_calculate_lufs(omega_ctx* c, const float* x, int64_t n_frames, int32_t
   }
   // The weighting and the true peak read the same input and write different outputs: the true peak
   // runs on the side stream beside the weighting's latency-bound float64 scans (per-call metering of
-  // the app's 2048-sample frames: 37 + 14 us of kernels in sequence before), both joined before the
-  // aggregates (whose ordering against the side stream omega_meter_update keeps as always).
+  // the app's 2048-sample frames: 37 + 14 us of kernels in sequence before). The aggregates read the
+  // meter state, which a meter prep on the side stream may still be writing, and the true peaks.
+  // Joining the side stream by an event costs ~5-10 us of idle GPU between kernels, so: when no meter
+  // kernel went to the side stream since the last join (the app's steady state: nothing but these
+  // calls; side_meters) there is nothing to join before, and the true peaks (power-of-two frames,
+  // direct launches) count themselves in on a device counter that the first meter prep polls before it
+  // reads them; otherwise events, as omega_meter_update.
+  const bool capture = c->cap && c->stream == c->cap;
+  const bool counted = !capture && is_pow2_in(m, 512, 16384);
+  if (counted && c->side_meters) {
+    HIPC(c, hipEventRecord(c->ev_join[1], c->fork[0]));
+    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[1], 0));
+  }
+  c->side_meters = false;
   HIPC(c, hipEventRecord(c->ev_fork, c->stream));
   HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
   {
     const hipStream_t main = c->stream;
     c->stream = c->fork[0];
+    c->tp_count_to = counted ? c->d_kw_done + 5 : nullptr;
     e = omega_true_peak_os(c, dx, ncf, m, oversampling, dt, OMEGA_MEM_DEVICE);
+    c->tp_count_to = nullptr;
     c->stream = main;
     if (e) return e;
   }
+  if (counted) c->lt_issued += (unsigned)ncf;
   if ((e = omega_weighting(c, dx, ncf, m, mode, nullptr, dl, OMEGA_MEM_DEVICE))) return e;
-  HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
-  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[0], 0));
-  if ((e = omega_meter_update(c, dl, dt, n_frames, dm, OMEGA_MEM_DEVICE))) return e;
-  if (mem == OMEGA_MEM_HOST) return finish_host(c, outs);
+  if (!counted) {
+    // the side stream's last work is the true peak, behind any earlier meter prep: one join serves
+    // both (omega_meter_update's second wait is skipped)
+    HIPC(c, hipEventRecord(c->ev_join[0], c->fork[0]));
+    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[0], 0));
+  }
+  if ((e = flush_meters(c))) return e;
+  // for a host-memory call the side stream is ordered after the copies back (no event between the
+  // aggregates and the copies)
+  const bool host = mem == OMEGA_MEM_HOST;
+  if ((e = meter_update_dev(c, dl, dt, n_frames, dm, false, !host, counted ? c->d_kw_done + 5 : nullptr,
+                            c->lt_issued)))
+    return e;
+  if (host) {
+    if ((e = finish_host(c, outs))) return e;
+    HIPC(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_fork, 0));
+    return 0;
+  }
   return 0;
 } catch (...) {
   return guard_fail(c);

@@ -265,7 +265,17 @@ __device__ __forceinline__ void truepeak_body(const SpectralParams& p, int64_t c
     OMEGA_STAMP(2 + 2 * P);
   }
   const float peak = block_max<NTH>(fmaxf(mx, fmx * (1.0f / K)), red, tid);
-  if (tid == 0) p.tp_out[cf] = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
+  if (tid == 0) {
+    const float db = peak < 1e-10f ? -100.0f : 20.0f * log10f(peak);
+    if (p.tp_done) {  // write-through, drained, then counted in (see SpectralParams::tp_done)
+      __hip_atomic_store(reinterpret_cast<unsigned*>(p.tp_out + cf), __float_as_uint(db), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(p.tp_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      p.tp_out[cf] = db;
+    }
+  }
   OMEGA_STAMP(9);
 }
 

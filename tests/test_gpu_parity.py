@@ -376,6 +376,38 @@ def test_calculate_lufs_fused_equals_three_calls():
         np.testing.assert_array_equal(met, met2)
 
 
+def test_calculate_lufs_interleaved_with_batches():
+    """omega_calculate_lufs joins the side stream by a device counter (its true peaks count in, the
+    first meter prep polls it) while only its own true peaks went there, and by an event once a batch's
+    meter prep did: calls interleaved with process_frames batches on one context, and repeated calls in
+    a row, give bitwise what the same sequence gives with the host synchronised after every call."""
+    import torch
+    from omega_gpu import Engine, NORTHSTAR_RESOLUTIONS
+    xb = torch.from_numpy(S.cfg2_batch(32, seed_l=21, seed_r=22)).cuda()
+    rng = np.random.default_rng(23)
+    xs = (0.2 * rng.standard_normal((9, 2, 2048))).astype(np.float32)
+    res = []
+    for sync in (False, True):
+        eng = Engine(NORTHSTAR_RESOLUTIONS, FS, 20000, target_bins=512, n_channels=2)
+        outs = []
+        for k in range(9):
+            if k in (0, 5):
+                o = eng.process_frames(xb[16 * (k // 5):16 * (k // 5) + 16], 16, 2 * 16384, 16384, meters=True)
+                if sync:
+                    eng.synchronize()
+                    torch.cuda.synchronize()
+                outs.append(o["meters"])
+            li, tp, met = eng.calculate_lufs(xs[k], "K")
+            outs.extend([li, tp, met])
+            if sync:
+                eng.synchronize()
+        eng.synchronize()
+        torch.cuda.synchronize()
+        res.append([o.cpu().numpy() if hasattr(o, "cpu") else o for o in outs])
+    for a, b in zip(*res):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_meter_too_short_keeps_state():
     """A frame of 9 samples or fewer (scipy's filtfilt raises: padlen 9) is logged and the meters keep
     their state; 480 samples (not a power of two) is metered like the reference."""

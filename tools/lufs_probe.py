@@ -12,8 +12,14 @@ import numpy as np  # noqa: E402
 
 
 def main():
+    args = sys.argv[1:]
+    if "--lib" in args:  # another build in lib/ (A/B of builds on one box)
+        i = args.index("--lib")
+        from omega_gpu import _lib
+        _lib.use_development_library(args[i + 1])
+        del args[i:i + 2]
     from omega_gpu.professional_meters import ProfessionalMetering
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+    n = int(args[0]) if args else 300
     rng = np.random.default_rng(8)
     frames = [(0.3 * np.sin(2 * np.pi * 440 * np.arange(2048) / 48000 + 0.1 * k) + 0.01 * rng.standard_normal(2048))
               * np.hanning(2048) for k in range(64)]
@@ -23,7 +29,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(n):
         pm.calculate_lufs(frames[k % 64])
-    print(f"calculate_lufs: {(time.perf_counter() - t0) / n * 1e3:.4f} ms per call")
+    print(f"calculate_lufs: {(time.perf_counter() - t0) / n * 1e3:.4f} ms per call ({' '.join(sys.argv[1:])})")
 
 
 if __name__ == "__main__":

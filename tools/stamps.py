@@ -29,7 +29,8 @@ def main(stage):
     getter = {"kw": "omega_debug_kw_stamps", "tp": "omega_debug_spectral_stamps", "tprf": "omega_debug_rf_stamps",
               "mrfft": "omega_debug_spectral_stamps", "meters": "omega_debug_meter_stamps",
               "spectra": "omega_debug_spectra_stamps", "spectra_rf": "omega_debug_rf_stamps",
-              "post": "omega_debug_post_stamps", "drum": "omega_debug_drum_stamps"}[stage]
+              "post": "omega_debug_post_stamps", "drum": "omega_debug_drum_stamps",
+              "w64": "omega_debug_w64_stamps"}[stage]
     if stage in ("spectra", "spectra_rf"):
         from omega_gpu import Resolution
         from omega_gpu.engine import BandTable
@@ -60,6 +61,9 @@ def main(stage):
                 xd = torch.from_numpy(np.abs(np.random.default_rng(5).standard_normal((4096, 1025))).astype(np.float32)).cuda()
                 od = torch.empty(4096, 14, dtype=torch.float64, device="cuda")
             eng.drum_features(xd, out=od)
+        elif stage == "w64":  # the calculate_lufs frame: one 2048-sample frame through the float64 K-weighting
+            x1 = np.ascontiguousarray((0.3 * np.sin(np.arange(2048) / 7.0) * np.hanning(2048)).astype(np.float32))
+            eng.weighting(x1[None, :], "K", weighted=False)
         elif stage == "meters":
             eng._check(lib.omega_meter_update(eng._ctx, li.data_ptr(), tpv.data_ptr(), 256, met.data_ptr(),
                                               L.MEM_DEVICE))
