@@ -242,7 +242,10 @@ int omega_meter_load_history(omega_ctx* ctx, const float* lufs_inst, int64_t n_l
  * and the meter aggregates (as omega_meter_update) for n_frames x n_channels channel-frames of length
  * m (frame-major, contiguous), with one host round trip when mem = OMEGA_MEM_HOST (the three entry
  * points each stage, launch and synchronize on their own). lufs_inst / tp_db may be NULL (device
- * scratch), meters [n_cf, 5] is required. */
+ * scratch), meters [n_cf, 5] is required. The true peak runs on the context's side stream beside the
+ * weighting; for power-of-two frame lengths it counts in on a device counter that the aggregates
+ * poll (bounded, OMEGA_EHIP on expiry), so the caller's stream joins the side stream by an event only
+ * when other meter work went there since the last call. Outputs are bitwise those of the three calls. */
 int omega_calculate_lufs(omega_ctx* ctx, const float* x, int64_t n_frames, int32_t m, int32_t mode,
                          int32_t oversampling, float* lufs_inst, float* tp_db, double* meters, int mem);
 
