@@ -1310,7 +1310,7 @@ int enqueue_batch(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int6
         p.wait_target = c->kw_issued;
       }
       HIPC(c, launch_meter_prep(p, c->fork[0]));
-    c->side_meters = true;
+      c->side_meters = true;
       p.parts = 1;
       p.q_done = c->d_kw_done + 1;
       HIPC(c, launch_meter_query(p, c->fork[0]));
@@ -1438,7 +1438,7 @@ int enqueue_frames(omega_ctx* c, SpectralParams sp, KWeightParams kp, int W, int
     HIPC(c, hipStreamWaitEvent(c->fork[0], c->ev_kw, 0));
     for (MeterPrepParams p : mc) {
       HIPC(c, launch_meter_prep(p, c->fork[0]));
-    c->side_meters = true;
+      c->side_meters = true;
       p.parts = 1;
       HIPC(c, launch_meter_query(p, c->fork[0]));
       c->side_meters = true;
